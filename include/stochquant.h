@@ -1,0 +1,152 @@
+/*
+ * stochquant.h -- C ABI of libstochquant.so, the MI355X-native (gfx950) drop-in
+ * for SebTanz/StochQuant's Langevin path.
+ *
+ * The reference has no library API: its host program tauhost.c drives one
+ * OpenCL kernel inline from main() (clCreateBuffer / clEnqueueWriteBuffer /
+ * clEnqueueNDRangeKernel / clEnqueueReadBuffer, tauhost.c:255-560) and its
+ * Python driver talks to that program over argv + stdout (taumain.py:132).
+ * Each entry point below names the reference code it replaces.  All functions
+ * are extern "C", take plain pointers and sizes, never throw, and return 0 on
+ * success or a negative SQ_E* code; sq_last_error() gives the message
+ * (thread-local).  A context is not thread-safe; the library owns all device
+ * memory, HIP streams and RCCL communicators; host arrays are only copied
+ * in/out and never retained.
+ */
+#ifndef STOCHQUANT_H
+#define STOCHQUANT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SQ_ABI_VERSION 1
+
+/* status codes */
+#define SQ_OK 0
+#define SQ_E_ARG -1      /* invalid argument / unsupported shape */
+#define SQ_E_HIP -2      /* HIP runtime error */
+#define SQ_E_COMM -3     /* RCCL / halo-exchange error */
+#define SQ_E_STATE -4    /* call not valid for this context's model/state */
+#define SQ_E_NODEV -5    /* no HIP device */
+
+/* models */
+#define SQ_MODEL_QM1D 0  /* the reference's 1-D chain + collective coordinate (tau_kernel.cl:25-175), fp64 */
+#define SQ_MODEL_PHI4 1  /* 3-D phi^4 lattice, fp32 (north-star extension) */
+
+/* halo transport for slab decomposition (SQ_MODEL_PHI4 only) */
+#define SQ_COMM_NONE 0      /* one slab, periodic z handled in-kernel */
+#define SQ_COMM_LOOPBACK 1  /* nslabs slabs on this device, halos by D2D copies */
+#define SQ_COMM_RCCL 2      /* one slab per process, halos by ncclSend/ncclRecv over xGMI */
+
+typedef struct sq_params {
+    int struct_size;            /* = sizeof(sq_params) */
+    int model;                  /* SQ_MODEL_* */
+    long long dims[3];          /* QM1D: {N,1,1} (argv[1]); PHI4: global {Lx, Ly, Lz} */
+    double deltat;              /* QM1D lattice spacing Δt (argv[2]); PHI4: unused (a = 1) */
+    double deltatau;            /* Langevin step Δτ (argv[3]) */
+    int pot;                    /* QM1D potID 0 = harmonic, 3 = double well (argv[5]) */
+    double C;                   /* noise amplitude (argv[6]) */
+    int loops;                  /* Langevin steps per frame (argv[10]) */
+    unsigned long long seed;    /* Philox key (tauhost.c:185 seeds from rand()) */
+    double m2, lambda;          /* PHI4: V = m2/2 phi^2 + lambda/24 phi^4 */
+    double clamp;               /* guard: |v| > clamp -> +-clamp, NaN -> clamp (tau_kernel.cl:119-133); 1000 */
+    int device;                 /* HIP device ordinal (argv[7] was an OpenCL platform index) */
+    int adapt_dtau;             /* 1: reference Δτ controller in sq_run_frame (tauhost.c:523-541) */
+    int comm;                   /* SQ_COMM_* */
+    int nranks, rank;           /* SQ_COMM_RCCL: processes, this process' rank */
+    int nslabs;                 /* SQ_COMM_LOOPBACK: slabs on this device */
+    unsigned char comm_id[128]; /* SQ_COMM_RCCL: ncclUniqueId from sq_comm_unique_id on rank 0 */
+} sq_params;
+
+typedef struct sq_perf_t {
+    long long steps;            /* Langevin steps executed since the last sq_perf_reset */
+    long long site_updates;     /* local sites x steps */
+    double step_kernel_ms;      /* sum of hipEvent-timed durations of the step kernels (profiling on) */
+    long long step_kernel_launches;
+    double frame_ms;            /* wall time inside sq_run_frame / sq_step (host clock) */
+    double halo_bytes;          /* bytes sent by halo exchange */
+} sq_perf_t;
+
+typedef struct sq_ctx sq_ctx;
+
+/* Defaults: QM1D, reference constants (clamp 1000, adapt_dtau 1, comm none). */
+void sq_params_init(sq_params *p);
+const char *sq_last_error(void);
+int sq_abi_version(void);
+
+/* Replaces the OpenCL context/queue/buffer/program/kernel set-up,
+ * tauhost.c:196-453 (clGetPlatformIDs ... clSetKernelArg). */
+int sq_create(const sq_params *p, sq_ctx **out);
+/* Replaces the clRelease* tail, tauhost.c:587-612. */
+int sq_destroy(sq_ctx *ctx);
+
+/* QM1D state upload: replaces the initial clEnqueueWriteBuffer calls
+ * tauhost.c:319-377 and the per-frame re-upload :550-554.  f, x, xx0 have N
+ * doubles; runs is the running-mean count (nr_mem_obj). */
+int sq_upload(sq_ctx *ctx, const double *f, const double *x, const double *xx0, double omega, long runs);
+/* QM1D state download: replaces clEnqueueReadBuffer of newf/newx/newxx0/omega,
+ * tauhost.c:508-515.  Any pointer may be NULL. */
+int sq_download(sq_ctx *ctx, double *f, double *x, double *xx0, double *omega, long *runs);
+/* QM1D carried stability-scan state (lrgEl/lrgVl, tauhost.c:65-66,350-354)
+ * and the Philox step counter; for tests and checkpoint/resume. */
+int sq_qm1d_get_scan(sq_ctx *ctx, int *lrgEl, double *lrgVl, unsigned long long *tick);
+int sq_qm1d_set_scan(sq_ctx *ctx, int lrgEl, double lrgVl, unsigned long long tick);
+
+/* One frame = `loops` Langevin steps (one clEnqueueNDRangeKernel + clFinish,
+ * tauhost.c:481-483) with the stability read-back :504-505, adoption of the
+ * new state on success :506-532, rollback to the frame-start snapshot on
+ * failure :533-554 (kept on device, no host round trip), and, if
+ * adapt_dtau, the reference Δτ controller :523-541. */
+int sq_run_frame(sq_ctx *ctx, int *stable);
+
+/* PHI4: raw Langevin steps without frame control (the bench's hot path). */
+int sq_step(sq_ctx *ctx, int nsteps);
+/* PHI4 field I/O of this process' slab(s): nz_local*Ly*Lx floats, z slowest. */
+int sq_upload_field(sq_ctx *ctx, const float *phi, size_t count);
+int sq_download_field(sq_ctx *ctx, float *phi, size_t count);
+/* PHI4: phi = amp * Philox normal(seed, stream 2, site), generated on device. */
+int sq_init_field(sq_ctx *ctx, float amp);
+/* PHI4 local slab geometry: nz_local and the global z of its first plane. */
+int sq_slab(sq_ctx *ctx, long long *nz_local, long long *z0);
+/* PHI4 observables over this process' slab: out[0] = sum phi, out[1] = sum
+ * phi^2, out[2] = max |phi| (double accumulation on device). */
+int sq_moments(sq_ctx *ctx, double out[3]);
+
+/* Δτ (dt_mem_obj, tauhost.c:346,526,540). */
+int sq_set_dtau(sq_ctx *ctx, double dtau);
+int sq_get_dtau(sq_ctx *ctx, double *dtau);
+int sq_get_step(sq_ctx *ctx, unsigned long long *step);
+int sq_set_step(sq_ctx *ctx, unsigned long long step);
+
+/* Correlator of the reference's observables: QM1D out[i] = xx0[i] -
+ * x[i]*x[mid] (host xavg, tauhost.c:519-521), n <= N.  PHI4: zero-momentum
+ * time-slice correlator over z, out[t] = <S(z) S(z+t)>/V, n <= Lz, where
+ * S(z) = sum_{x,y} phi (single-slab contexts). */
+int sq_correlator(sq_ctx *ctx, double *out, int n);
+
+/* Profiling: per-launch hipEvents around every step kernel on its stream. */
+int sq_set_profiling(sq_ctx *ctx, int on);
+int sq_perf(sq_ctx *ctx, sq_perf_t *out);
+int sq_perf_reset(sq_ctx *ctx);
+int sq_sync(sq_ctx *ctx);
+
+/* RCCL bootstrap: rank 0 creates the id, the caller distributes it (e.g. via
+ * torch.distributed) into sq_params.comm_id of every rank. */
+int sq_comm_unique_id(unsigned char out[128]);
+
+/* Device queries / self-tests used by tests and bench (no reference analogue). */
+int sq_device_count(int *n);
+int sq_selftest_normals(int device, unsigned long long seed, unsigned int stream,
+                        unsigned long long quad0, unsigned long long step, float *out, size_t nquads);
+int sq_selftest_dpp(int device, float *out64x2);
+int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
+int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STOCHQUANT_H */

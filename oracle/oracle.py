@@ -1,0 +1,139 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module, and only as the checker (or the timed CPU baseline).
+The product never routes through it.  See sq_oracle.h for what each
+restatement follows in the reference.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+CLI = os.path.join(HERE, "orc_tauhost")
+
+_D = ctypes.POINTER(ctypes.c_double)
+_F = ctypes.POINTER(ctypes.c_float)
+_U32 = ctypes.POINTER(ctypes.c_uint32)
+
+
+class Qm1d(ctypes.Structure):
+    _fields_ = [
+        ("N", ctypes.c_int), ("pot", ctypes.c_int), ("loops", ctypes.c_int),
+        ("a", ctypes.c_double), ("c", ctypes.c_double), ("dtau", ctypes.c_double),
+        ("seed", ctypes.c_uint64), ("tick", ctypes.c_uint64), ("runs", ctypes.c_int),
+        ("f", _D), ("x", _D), ("xx0", _D), ("nf", _D), ("nx", _D), ("nxx0", _D),
+        ("omega", ctypes.c_double), ("nomega", ctypes.c_double),
+        ("lrgEl", ctypes.c_int), ("lrgVl", ctypes.c_double),
+        ("stable", ctypes.c_int), ("steps_done", ctypes.c_int),
+    ]
+
+
+class Phi4(ctypes.Structure):
+    _fields_ = [
+        ("Lx", ctypes.c_int), ("Ly", ctypes.c_int), ("Lz", ctypes.c_int),
+        ("h", ctypes.c_float), ("m2", ctypes.c_float), ("lam", ctypes.c_float), ("clampv", ctypes.c_float),
+        ("seed", ctypes.c_uint64), ("C", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def build():
+    r = subprocess.run(["make", "-C", HERE, "-j4"], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(r.stdout + r.stderr)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.orc_philox4x32_10.argtypes = [_U32, _U32, _U32]
+        L.orc_normals4.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _F]
+        L.orc_xcl.restype = ctypes.c_double
+        L.orc_xcl.argtypes = [ctypes.c_double, ctypes.c_double, ctypes.c_int]
+        L.orc_intconst.restype = ctypes.c_double
+        L.orc_intconst.argtypes = [ctypes.c_int]
+        L.orc_qm1d_frame.argtypes = [ctypes.POINTER(Qm1d)]
+        L.orc_phi4_step.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_uint64, ctypes.c_int]
+        L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
+                                         ctypes.c_uint64]
+        L.orc_phi4_init.argtypes = [ctypes.POINTER(Phi4), ctypes.c_float, _F]
+        L.orc_phi4_sigma.restype = ctypes.c_float
+        L.orc_phi4_sigma.argtypes = [ctypes.c_float, ctypes.c_double]
+        _lib = L
+    return _lib
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().orc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def normals(seed, stream, quad0, step, nquads):
+    out = np.empty(4 * nquads, dtype=np.float32)
+    L = lib()
+    tmp = (ctypes.c_float * 4)()
+    for q in range(nquads):
+        L.orc_normals4(seed, stream, quad0 + q, step, tmp)
+        out[4 * q:4 * q + 4] = tmp[:]
+    return out
+
+
+def qm1d_frame(N, a, dtau, pot, C, loops, seed, tick, runs, f, x, xx0, omega, lrgEl=0, lrgVl=0.0):
+    """One Jacobi-semantics frame (the GPU's contract); returns a dict."""
+    f = np.ascontiguousarray(f, dtype=np.float64)
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    xx0 = np.ascontiguousarray(xx0, dtype=np.float64)
+    nf, nx, nxx0 = np.empty(N), np.empty(N), np.empty(N)
+    s = Qm1d(N=N, pot=pot, loops=loops, a=a, c=C, dtau=dtau, seed=seed, tick=tick, runs=runs,
+             f=f.ctypes.data_as(_D), x=x.ctypes.data_as(_D), xx0=xx0.ctypes.data_as(_D),
+             nf=nf.ctypes.data_as(_D), nx=nx.ctypes.data_as(_D), nxx0=nxx0.ctypes.data_as(_D),
+             omega=omega, lrgEl=lrgEl, lrgVl=lrgVl)
+    lib().orc_qm1d_frame(ctypes.byref(s))
+    return {"f": nf, "x": nx, "xx0": nxx0, "omega": s.nomega, "lrgEl": s.lrgEl, "lrgVl": s.lrgVl,
+            "stable": s.stable, "steps_done": s.steps_done}
+
+
+def phi4_params(shape, h, m2, lam, seed, clamp=1000.0, C=1.0):
+    Lx, Ly, Lz = shape
+    return Phi4(Lx=Lx, Ly=Ly, Lz=Lz, h=h, m2=m2, lam=lam, clampv=clamp, seed=seed, C=C)
+
+
+def phi4_step(p, phi, step, nthreads=0):
+    a = np.ascontiguousarray(phi, dtype=np.float32)
+    out = np.empty_like(a)
+    lib().orc_phi4_step(ctypes.byref(p), a.ctypes.data_as(_F), out.ctypes.data_as(_F), step, nthreads)
+    return out
+
+
+def phi4_step_slab(p, padded, z0, step):
+    """padded: (nz+2, Ly, Lx) with ghost planes; returns the nz updated planes."""
+    a = np.ascontiguousarray(padded, dtype=np.float32)
+    nz = a.shape[0] - 2
+    out = np.empty((nz,) + a.shape[1:], dtype=np.float32)
+    lib().orc_phi4_step_slab(ctypes.byref(p), a.ctypes.data_as(_F), out.ctypes.data_as(_F), nz, z0, step)
+    return out
+
+
+def phi4_init(p, amp):
+    out = np.empty((p.Lz, p.Ly, p.Lx), dtype=np.float32)
+    lib().orc_phi4_init(ctypes.byref(p), amp, out.ctypes.data_as(_F))
+    return out
+
+
+def tauhost(argv, cwd):
+    """Run the serial-reference-semantics CLI (orc_tauhost) with tauhost.c's argv."""
+    if not os.path.exists(CLI):
+        build()
+    return subprocess.run([CLI] + [str(a) for a in argv], cwd=cwd, capture_output=True, timeout=300)

@@ -1,0 +1,104 @@
+/*
+ * orc_phi4.c -- oracle for the north-star 3-D extension (TEST INFRASTRUCTURE
+ * ONLY, see sq_oracle.h; also bench.py's cpu_baseline, kind "port").
+ *
+ * The reference's per-site update (tau_kernel.cl:111-117: old value + Δτ ×
+ * (lattice Laplacian − V'') + noise, then the ±max / NaN guard :119-133)
+ * generalised to a periodic 3-D fp32 lattice with the full non-linear force
+ * of V(φ) = ½ m² φ² + (λ/4!) φ⁴ (SURVEY.md §8a "Build-side hot-path unit"):
+ *
+ *   nb   = ((φ[x-1] + φ[x+1]) + (φ[y-1] + φ[y+1])) + (φ[z-1] + φ[z+1])
+ *   lap  = fma(-6, φ, nb)
+ *   g    = fma(λ/6, φ·φ, m²)
+ *   drift= fma(-φ, g, lap)
+ *   φ'   = fma(σ, ξ, fma(Δτ, drift, φ)),     σ = C·sqrt(2Δτ) (C = 1 physical)
+ *   φ'   = NaN ? max : clamp(φ', -max, max)
+ *
+ * The evaluation order is the product's (fp32, explicit fma); the only
+ * GPU-vs-oracle difference is ξ, whose hardware transcendentals are compared
+ * with the double-evaluated value here under the tolerance stated in
+ * tests/test_gpu_parity.py.  Site index s = (z·Ly + y)·Lx + x (global),
+ * noise quad s>>2, component s&3, stream 0.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include "sq_oracle.h"
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+float orc_phi4_sigma(float h, double C) { return (float)(sqrt(2.0 * (double)h) * C); }
+float orc_phi4_lam6(float lam) { return (float)((double)lam / 6.0); }
+
+/* One plane of the update: c = plane z, zm/zp = planes z-1, z+1 (already
+ * resolved by the caller: periodic wrap or ghost planes), zg = global z. */
+static void phi4_plane(const orc_phi4 *p, const float *cz, const float *czmp, const float *czpp,
+                       float *oz, uint64_t zg, uint64_t step)
+{
+    const int Lx = p->Lx, Ly = p->Ly;
+    const float h = p->h, m2 = p->m2, lam6 = orc_phi4_lam6(p->lam);
+    const float sig = orc_phi4_sigma(h, p->C), mx = p->clampv;
+    for (int y = 0; y < Ly; ++y) {
+        const int ym = (y + Ly - 1) % Ly, yp = (y + 1) % Ly;
+        const float *c = cz + (size_t)y * Lx;
+        const float *cym = cz + (size_t)ym * Lx;
+        const float *cyp = cz + (size_t)yp * Lx;
+        const float *czm = czmp + (size_t)y * Lx;
+        const float *czp = czpp + (size_t)y * Lx;
+        float *o = oz + (size_t)y * Lx;
+        const uint64_t row0 = (zg * (uint64_t)Ly + (uint64_t)y) * (uint64_t)Lx;
+        for (int x0 = 0; x0 < Lx; x0 += 4) {
+            float xi[4];
+            orc_normals4(p->seed, 0, (row0 + (uint64_t)x0) >> 2, step, xi);
+            for (int k = 0; k < 4; ++k) {
+                const int x = x0 + k;
+                const int xm = (x + Lx - 1) % Lx, xp = (x + 1) % Lx;
+                const float phi = c[x];
+                const float nb = ((c[xm] + c[xp]) + (cym[x] + cyp[x])) + (czm[x] + czp[x]);
+                const float lap = fmaf(-6.0f, phi, nb);
+                const float g = fmaf(lam6, phi * phi, m2);
+                const float drift = fmaf(-phi, g, lap);
+                float v = fmaf(sig, xi[k], fmaf(h, drift, phi));
+                v = isnan(v) ? mx : (v > mx ? mx : (v < -mx ? -mx : v));
+                o[x] = v;
+            }
+        }
+    }
+}
+
+void orc_phi4_step(const orc_phi4 *p, const float *in, float *out, uint64_t step, int nthreads)
+{
+    const int Lz = p->Lz;
+    const size_t plane = (size_t)p->Lx * p->Ly;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int z = 0; z < Lz; ++z) {
+        const int zm = (z + Lz - 1) % Lz, zp = (z + 1) % Lz;
+        phi4_plane(p, in + (size_t)z * plane, in + (size_t)zm * plane, in + (size_t)zp * plane,
+                   out + (size_t)z * plane, (uint64_t)z, step);
+    }
+}
+
+/* Slab form used by the decomposition tests: `in` holds nz+2 planes (ghost,
+ * slab, ghost), `out` the nz updated planes; z0 = global z of slab plane 0. */
+void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, uint64_t z0,
+                        uint64_t step)
+{
+    const size_t plane = (size_t)p->Lx * p->Ly;
+    for (int z = 0; z < nz; ++z)
+        phi4_plane(p, in + (size_t)(z + 1) * plane, in + (size_t)z * plane, in + (size_t)(z + 2) * plane,
+                   out + (size_t)z * plane, z0 + (uint64_t)z, step);
+}
+
+void orc_phi4_init(const orc_phi4 *p, float amp, float *out)
+{
+    const size_t n = (size_t)p->Lx * p->Ly * p->Lz;
+    for (size_t s = 0; s < n; s += 4) {
+        float xi[4];
+        orc_normals4(p->seed, 2, (uint64_t)(s >> 2), 0, xi);
+        for (int k = 0; k < 4 && s + k < n; ++k) out[s + k] = amp * xi[k];
+    }
+}

@@ -1,0 +1,113 @@
+/*
+ * sq_oracle.h -- CPU restatement of SebTanz/StochQuant's Langevin path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product:
+ * only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker (or the timed CPU baseline),
+ * never as the thing measured or shipped.
+ *
+ * Three restatements live here:
+ *
+ *  1. "serial" QM1D  -- the reference's exact semantics under a serialising
+ *     OpenCL runtime (work-items 0..N in id order between barriers, one shared
+ *     48-bit LCG), restating tau_kernel.cl:25-175 + :184-284 and the host
+ *     frame loop tauhost.c:29-581.  Pinned against the only reference outputs
+ *     that exist (recorded during the survey from the
+ *     reference's unmodified sources); see tests/golden/README.md.
+ *
+ *  2. "jacobi" QM1D  -- the same update with Jacobi ordering, counter-based
+ *     Philox4x32-10 noise and an order-independent statement of the stability
+ *     scan.  This is the semantics the HIP kernel implements; parity of the GPU
+ *     against the reference is therefore: (i) bitwise for the deterministic
+ *     part (C = 0, potID 0), (ii) a stated fp tolerance otherwise, (iii)
+ *     statistical observables.  The reference's own trajectory is defined only
+ *     under one serialisation, so bitwise GPU-vs-reference
+ *     trajectory parity is impossible by construction.
+ *
+ *  3. "phi4" 3-D     -- the north-star extension: fp32 φ⁴ Jacobi Langevin step
+ *     on a periodic Lx×Ly×Lz lattice, same Philox noise.  Also the CPU baseline
+ *     of bench.py (OpenMP over host cores, kind "port").
+ */
+#ifndef SQ_ORACLE_H
+#define SQ_ORACLE_H
+#include <stdint.h>
+#include <stdio.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- RNG ---------------- */
+/* Philox4x32-10 (Salmon et al., SC'11, "Random123"), published algorithm. */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* Four standard normals for (seed, stream, quad, step); layout in DESIGN.md §RNG. */
+void orc_normals4(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4]);
+/* The reference's shared-seed LCG + Box-Muller, tau_kernel.cl:269-284. */
+double orc_ref_random(uint64_t *seed, int gid);
+
+/* ---------------- physics helpers (tau_kernel.cl:184-267) ---------------- */
+double orc_xcl(double t, double w, int pot);
+double orc_ddpot(double x, int pot);
+double orc_intconst(int pot);
+
+/* ---------------- serial (reference-order) QM1D ---------------- */
+typedef struct {
+    int N, pot, loops;
+    double a, c;
+    double *f, *x, *xx0, *nf, *nx, *nxx0; /* "device" buffers, length N */
+    double omega;
+    uint64_t seed;   /* rand1 */
+    int stable;
+    double dtau;     /* dt_mem_obj */
+    int lrgEl;
+    double lrgVl;
+    int runs;        /* nr_mem_obj */
+} orc_serial_dev;
+
+/* One clEnqueueNDRangeKernel of time_dev with global size N+1 (single WG). */
+void orc_serial_launch(orc_serial_dev *d);
+
+/* The whole of tauhost.c main() (argv[1..13]) with the serial kernel in place
+ * of OpenCL.  stdout lines go to `out`; returns the process exit code. */
+int orc_tauhost_main(int argc, const char **argv, FILE *out);
+
+/* ---------------- Jacobi QM1D (the GPU's semantics) ---------------- */
+typedef struct {
+    int N, pot, loops;
+    double a, c, dtau;
+    uint64_t seed;
+    uint64_t tick;   /* attempted-step counter = Philox step index */
+    int runs;
+    double *f, *x, *xx0;        /* in: frame-start state */
+    double *nf, *nx, *nxx0;     /* out: state after the frame */
+    double omega, nomega;
+    int lrgEl; double lrgVl;    /* carried across frames, not rolled back */
+    int stable;
+    int steps_done;
+} orc_qm1d;
+
+void orc_qm1d_frame(orc_qm1d *s);
+
+/* ---------------- φ⁴ 3-D (fp32) ---------------- */
+typedef struct {
+    int Lx, Ly, Lz;
+    float h, m2, lam, clampv;
+    uint64_t seed;
+    double C;        /* noise amplitude: sigma = (float)(sqrt(2h) * C) */
+} orc_phi4;
+
+/* One Jacobi Langevin step in -> out at noise step index `step`.
+ * nthreads <= 0: OpenMP default. */
+void orc_phi4_step(const orc_phi4 *p, const float *in, float *out, uint64_t step, int nthreads);
+/* Slab with explicit ghost planes: in = nz+2 planes, out = nz planes. */
+void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, uint64_t z0, uint64_t step);
+/* Derived float parameters exactly as the product computes them. */
+float orc_phi4_sigma(float h, double C);
+float orc_phi4_lam6(float lam);
+/* Initial field: phi = amp * normal(seed, stream 2, quad, step 0). */
+void orc_phi4_init(const orc_phi4 *p, float amp, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

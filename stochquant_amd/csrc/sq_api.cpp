@@ -1,0 +1,904 @@
+// sq_api.cpp -- C ABI of libstochquant.so (include/stochquant.h).
+//
+// Replaces the OpenCL host plumbing of tauhost.c (buffers, kernel args, the
+// per-frame launch / read-back / rollback / re-upload, tauhost.c:196-560) with
+// a library that owns device memory, HIP streams and RCCL communicators:
+//   * QM1D: frame-start state and frame result live in two device buffer sets;
+//     a stable frame flips the set, an unstable one simply keeps the old set
+//     (rollback without the reference's 3N+1-double host round trip).
+//   * PHI4: a slab per process (RCCL) or several slabs per device (loopback),
+//     each a padded ping-pong pair; per step the interior planes update on
+//     stream A while the halo exchange and the two boundary planes run on
+//     stream B, joined by events.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/stochquant.h"
+#include "sq_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define SQ_HIP(expr)                                                                             \
+    do {                                                                                         \
+        hipError_t e_ = (expr);                                                                  \
+        if (e_ != hipSuccess)                                                                    \
+            return fail(SQ_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+    } while (0)
+
+#define SQ_NCCL(expr)                                                                            \
+    do {                                                                                         \
+        ncclResult_t r_ = (expr);                                                                \
+        if (r_ != ncclSuccess)                                                                   \
+            return fail(SQ_E_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_));        \
+    } while (0)
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct Slab {
+    float *buf[2] = {nullptr, nullptr};  // padded ping-pong
+    float *snap = nullptr;               // frame-start snapshot (interior planes)
+    int nz = 0;
+    long long z0 = 0;
+    hipStream_t sA = nullptr, sB = nullptr;
+    hipEvent_t evA = nullptr, evB = nullptr, evPush = nullptr;
+};
+
+struct EvPair {
+    hipEvent_t a, b;
+};
+
+double host_intconst(int pot) {  // tau_kernel.cl:196-200,237-246 (float arithmetic)
+    if (pot == 3)
+        return (double)(sqrtf((float)3.) * powf((float)2., (float)(-5. / 4.)) *
+                        powf((float)2., (float)(-1. / 4.)) / sqrtf((float).8));
+    return 0.;
+}
+
+}  // namespace
+
+struct sq_ctx {
+    sq_params p{};
+    int dev = 0;
+    double dtau = 0;
+    int stab_cnt = 0;
+    unsigned long long step = 0;  // Philox step counter (attempted steps)
+    // QM1D
+    int N = 0;
+    double *qf[2] = {nullptr, nullptr}, *qx[2] = {nullptr, nullptr}, *qxx0[2] = {nullptr, nullptr};
+    int qcur = 0;
+    sq::Qm1dState *qst = nullptr;
+    double omega = 0;
+    long runs = 0;
+    int lrgEl = 0;
+    double lrgVl = 0;
+    hipStream_t qstream = nullptr;
+    // PHI4
+    int Lx = 0, Ly = 0;
+    long long Lz = 0;
+    sq::Phi4Geom geom{};
+    int zc = 8;
+    std::vector<Slab> slabs;
+    int cur = 0;
+    int *flag = nullptr;
+    double *dacc = nullptr;
+    unsigned int *dmax = nullptr;
+    ncclComm_t comm = nullptr;
+    // profiling
+    bool profiling = false;
+    std::vector<EvPair> evpool;
+    size_t ev_used = 0;
+    sq_perf_t perf{};
+};
+
+namespace {
+
+bool is_phi4(const sq_ctx *c) { return c->p.model == SQ_MODEL_PHI4; }
+
+int flush_events(sq_ctx *c) {
+    for (size_t i = 0; i < c->ev_used; ++i) {
+        SQ_HIP(hipEventSynchronize(c->evpool[i].b));
+        float ms = 0;
+        SQ_HIP(hipEventElapsedTime(&ms, c->evpool[i].a, c->evpool[i].b));
+        c->perf.step_kernel_ms += ms;
+        c->perf.step_kernel_launches += 1;
+    }
+    c->ev_used = 0;
+    return SQ_OK;
+}
+
+int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
+    *out = nullptr;
+    if (!c->profiling) return SQ_OK;
+    if (c->ev_used == c->evpool.size()) {
+        if (c->evpool.size() >= 8192) {
+            int rc = flush_events(c);
+            if (rc) return rc;
+        } else {
+            EvPair e;
+            SQ_HIP(hipEventCreate(&e.a));
+            SQ_HIP(hipEventCreate(&e.b));
+            c->evpool.push_back(e);
+        }
+    }
+    EvPair *e = &c->evpool[c->ev_used++];
+    SQ_HIP(hipEventRecord(e->a, s));
+    *out = e;
+    return SQ_OK;
+}
+
+sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s) {
+    sq::Phi4StepArgs a{};
+    a.in = s.buf[c->cur];
+    a.out = s.buf[c->cur ^ 1];
+    a.Lx = c->Lx;
+    a.Ly = c->Ly;
+    a.nz = s.nz;
+    a.zg0 = s.z0;
+    const float h = (float)c->dtau;
+    a.h = h;
+    a.m2 = (float)c->p.m2;
+    a.lam6 = (float)((double)(float)c->p.lambda / 6.0);
+    a.sig = (float)(sqrt(2.0 * (double)h) * c->p.C);  // sigma = C*sqrt(2 dtau) (tau_kernel.cl:112, a = 1)
+    a.clampv = (float)c->p.clamp;
+    a.k0 = (uint32_t)c->p.seed;
+    a.k1 = (uint32_t)(c->p.seed >> 32);
+    a.s_lo = (uint32_t)c->step;
+    a.s_hi = (uint32_t)(c->step >> 32);
+    a.flag = c->flag;
+    return a;
+}
+
+int phi4_launch_range(sq_ctx *c, const Slab &s, hipStream_t st, int zlo, int zhi, int zstep,
+                      int zc, int nzc, int periodic, bool timed) {
+    sq::Phi4StepArgs a = phi4_base_args(c, s);
+    a.zlo = zlo;
+    a.zhi = zhi;
+    a.zstep = zstep;
+    a.zc = zc;
+    a.nzc = nzc;
+    a.periodic = periodic;
+    sq::phi4_fill_units(a, c->geom);
+    EvPair *e = nullptr;
+    if (timed) {
+        int rc = ev_begin(c, st, &e);
+        if (rc) return rc;
+    }
+    SQ_HIP(sq::phi4_step_launch(a, c->geom, st));
+    if (e) SQ_HIP(hipEventRecord(e->b, st));
+    return SQ_OK;
+}
+
+size_t plane_floats(const sq_ctx *c) { return (size_t)c->Lx * (size_t)c->Ly; }
+
+// One Langevin step of every slab.
+int phi4_one_step(sq_ctx *c) {
+    const size_t plane = plane_floats(c);
+    const size_t pbytes = plane * sizeof(float);
+    if (c->p.comm == SQ_COMM_NONE) {
+        Slab &s = c->slabs[0];
+        const int nzc = (s.nz + c->zc - 1) / c->zc;
+        int rc = phi4_launch_range(c, s, s.sA, 0, s.nz, c->zc, c->zc, nzc, 1, true);
+        if (rc) return rc;
+    } else {
+        const int ns = (int)c->slabs.size();
+        // 1. halo exchange into the ghosts of the CURRENT buffers (stream B)
+        if (c->p.comm == SQ_COMM_LOOPBACK) {
+            for (int i = 0; i < ns; ++i) {
+                Slab &s = c->slabs[i];
+                Slab &dn = c->slabs[(i + ns - 1) % ns];
+                Slab &up = c->slabs[(i + 1) % ns];
+                float *cur = s.buf[c->cur];
+                // my plane 0 -> lower neighbour's upper ghost; my top plane -> upper's lower ghost
+                SQ_HIP(hipMemcpyAsync(dn.buf[c->cur] + (size_t)(dn.nz + 1) * plane, cur + plane,
+                                      pbytes, hipMemcpyDeviceToDevice, s.sB));
+                SQ_HIP(hipMemcpyAsync(up.buf[c->cur], cur + (size_t)s.nz * plane, pbytes,
+                                      hipMemcpyDeviceToDevice, s.sB));
+                SQ_HIP(hipEventRecord(s.evPush, s.sB));
+                c->perf.halo_bytes += 2.0 * (double)pbytes;
+            }
+            for (int i = 0; i < ns; ++i) {
+                Slab &s = c->slabs[i];
+                SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evPush, 0));
+                SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evPush, 0));
+            }
+        } else {  // RCCL: one slab per process
+            Slab &s = c->slabs[0];
+            float *cur = s.buf[c->cur];
+            const int P = c->p.nranks, r = c->p.rank;
+            const int up = (r + 1) % P, dn = (r + P - 1) % P;
+            SQ_NCCL(ncclGroupStart());
+            SQ_NCCL(ncclSend(cur + (size_t)s.nz * plane, plane, ncclFloat32, up, c->comm, s.sB));
+            SQ_NCCL(ncclSend(cur + plane, plane, ncclFloat32, dn, c->comm, s.sB));
+            SQ_NCCL(ncclRecv(cur, plane, ncclFloat32, dn, c->comm, s.sB));
+            SQ_NCCL(ncclRecv(cur + (size_t)(s.nz + 1) * plane, plane, ncclFloat32, up, c->comm, s.sB));
+            SQ_NCCL(ncclGroupEnd());
+            c->perf.halo_bytes += 2.0 * (double)pbytes;
+        }
+        // 2. boundary planes on B (after the interior kernel of the previous step read them)
+        for (auto &s : c->slabs) {
+            SQ_HIP(hipStreamWaitEvent(s.sB, s.evA, 0));
+            const int nzc = s.nz > 1 ? 2 : 1;
+            int rc = phi4_launch_range(c, s, s.sB, 0, s.nz, std::max(1, s.nz - 1), 1, nzc, 0, false);
+            if (rc) return rc;
+        }
+        // 3. interior planes on A (after the boundary kernel of the previous step)
+        for (auto &s : c->slabs) {
+            SQ_HIP(hipStreamWaitEvent(s.sA, s.evB, 0));
+            if (s.nz > 2) {
+                const int n = s.nz - 2;
+                const int nzc = (n + c->zc - 1) / c->zc;
+                int rc = phi4_launch_range(c, s, s.sA, 1, s.nz - 1, c->zc, c->zc, nzc, 0, true);
+                if (rc) return rc;
+            }
+            SQ_HIP(hipEventRecord(s.evA, s.sA));
+        }
+        for (auto &s : c->slabs) SQ_HIP(hipEventRecord(s.evB, s.sB));
+    }
+    c->cur ^= 1;
+    c->step += 1;
+    c->perf.steps += 1;
+    for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane;
+    return SQ_OK;
+}
+
+int phi4_join(sq_ctx *c) {
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipStreamSynchronize(s.sA));
+        SQ_HIP(hipStreamSynchronize(s.sB));
+    }
+    return SQ_OK;
+}
+
+int create_phi4(sq_ctx *c) {
+    const sq_params &p = c->p;
+    if (p.dims[0] <= 0 || p.dims[1] <= 0 || p.dims[2] <= 0 || p.dims[0] > (1 << 20) ||
+        p.dims[1] > (1 << 20))
+        return fail(SQ_E_ARG, "PHI4 dims must be positive");
+    c->Lx = (int)p.dims[0];
+    c->Ly = (int)p.dims[1];
+    c->Lz = p.dims[2];
+    if (!sq::phi4_geometry(c->Lx, c->Ly, &c->geom))
+        return fail(SQ_E_ARG, "PHI4 needs Lx in {8,16,32,64,128,256} or a multiple of 256, and Ly a "
+                              "multiple of the wave's row count");
+    if ((long long)c->Lx * c->Ly * c->Lz / 4 >= (1ll << 56))
+        return fail(SQ_E_ARG, "lattice too large for the Philox counter layout");
+    int nslab = 1;
+    long long zfirst = 0;
+    std::vector<long long> zs;
+    if (p.comm == SQ_COMM_NONE) {
+        zs = {0, c->Lz};
+    } else if (p.comm == SQ_COMM_LOOPBACK) {
+        nslab = p.nslabs;
+        if (nslab < 1 || nslab > c->Lz) return fail(SQ_E_ARG, "nslabs must be in [1, Lz]");
+        for (int i = 0; i <= nslab; ++i) zs.push_back(c->Lz * i / nslab);
+    } else if (p.comm == SQ_COMM_RCCL) {
+        if (p.nranks < 1 || p.rank < 0 || p.rank >= p.nranks || p.nranks > c->Lz)
+            return fail(SQ_E_ARG, "bad rank/nranks for RCCL slab decomposition");
+        zfirst = c->Lz * p.rank / p.nranks;
+        zs = {zfirst, c->Lz * (p.rank + 1) / p.nranks};
+    } else {
+        return fail(SQ_E_ARG, "unknown comm");
+    }
+    const size_t plane = plane_floats(c);
+    for (int i = 0; i < nslab; ++i) {
+        Slab s;
+        s.z0 = zs[i];
+        s.nz = (int)(zs[i + 1] - zs[i]);
+        if (s.nz < 1) return fail(SQ_E_ARG, "empty slab");
+        const size_t bytes = (size_t)(s.nz + 2) * plane * sizeof(float);
+        for (int k = 0; k < 2; ++k) {
+            SQ_HIP(hipMalloc(&s.buf[k], bytes));
+            SQ_HIP(hipMemset(s.buf[k], 0, bytes));
+        }
+        SQ_HIP(hipStreamCreateWithFlags(&s.sA, hipStreamNonBlocking));
+        SQ_HIP(hipStreamCreateWithFlags(&s.sB, hipStreamNonBlocking));
+        SQ_HIP(hipEventCreateWithFlags(&s.evA, hipEventDisableTiming));
+        SQ_HIP(hipEventCreateWithFlags(&s.evB, hipEventDisableTiming));
+        SQ_HIP(hipEventCreateWithFlags(&s.evPush, hipEventDisableTiming));
+        SQ_HIP(hipEventRecord(s.evA, s.sA));
+        SQ_HIP(hipEventRecord(s.evB, s.sB));
+        c->slabs.push_back(s);
+    }
+    SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
+    SQ_HIP(hipMemset(c->flag, 0, sizeof(int)));
+    SQ_HIP(hipMalloc(&c->dacc, 2 * sizeof(double)));
+    SQ_HIP(hipMalloc(&c->dmax, sizeof(unsigned int)));
+    if (p.comm == SQ_COMM_RCCL) {
+        ncclUniqueId id;
+        static_assert(sizeof(id.internal) <= 128, "ncclUniqueId size");
+        memcpy(id.internal, p.comm_id, sizeof(id.internal));
+        SQ_NCCL(ncclCommInitRank(&c->comm, p.nranks, id, p.rank));
+    }
+    // z chunk per wave: long enough to amortise the chunk-edge planes, short
+    // enough to give >= ~8 waves per CU.
+    const long long rows = (long long)(c->Lx / (4 * c->geom.qx)) * (c->Ly / c->geom.wy);
+    const int nz_max = c->slabs[0].nz;
+    int zc = 8;
+    while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
+    while (zc < 64 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 8192) zc *= 2;
+    if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
+    c->zc = zc;
+    return SQ_OK;
+}
+
+int create_qm1d(sq_ctx *c) {
+    const sq_params &p = c->p;
+    if (p.dims[0] < 2 || p.dims[0] > (1 << 30)) return fail(SQ_E_ARG, "QM1D needs N >= 2");
+    c->N = (int)p.dims[0];
+    if (sq::qm1d_sites_per_thread(c->N) == 0)
+        return fail(SQ_E_ARG, "QM1D single-workgroup kernel supports N <= 8192");
+    if (p.pot != 0 && p.pot != 3) return fail(SQ_E_ARG, "potID must be 0 or 3 (tau_kernel.cl:215-246)");
+    if (!(p.deltat > 0)) return fail(SQ_E_ARG, "deltat must be > 0");
+    if (p.loops < 1) return fail(SQ_E_ARG, "loops must be >= 1");
+    const size_t bytes = sizeof(double) * (size_t)c->N;
+    for (int k = 0; k < 2; ++k) {
+        SQ_HIP(hipMalloc(&c->qf[k], bytes));
+        SQ_HIP(hipMalloc(&c->qx[k], bytes));
+        SQ_HIP(hipMalloc(&c->qxx0[k], bytes));
+        SQ_HIP(hipMemset(c->qf[k], 0, bytes));
+        SQ_HIP(hipMemset(c->qx[k], 0, bytes));
+        SQ_HIP(hipMemset(c->qxx0[k], 0, bytes));
+    }
+    SQ_HIP(hipMalloc(&c->qst, sizeof(sq::Qm1dState)));
+    SQ_HIP(hipStreamCreateWithFlags(&c->qstream, hipStreamNonBlocking));
+    return SQ_OK;
+}
+
+int qm1d_frame(sq_ctx *c, int *stable) {
+    sq::Qm1dArgs a{};
+    const int k = c->qcur;
+    a.f = c->qf[k];
+    a.x = c->qx[k];
+    a.xx0 = c->qxx0[k];
+    a.nf = c->qf[k ^ 1];
+    a.nx = c->qx[k ^ 1];
+    a.nxx0 = c->qxx0[k ^ 1];
+    a.st = c->qst;
+    a.N = c->N;
+    a.pot = c->p.pot;
+    a.loops = c->p.loops;
+    a.runs = (int)c->runs;
+    a.a = c->p.deltat;
+    const float fa = (float)c->p.deltat;
+    a.a2 = (double)(fa * fa);
+    a.h = c->dtau;
+    a.sig = c->p.C * (double)sqrtf((float)(2. * c->dtau / c->p.deltat));
+    a.sigw = c->p.C * (double)sqrtf((float)(2. * c->dtau));
+    a.kconst = host_intconst(c->p.pot);
+    a.k0 = (uint32_t)c->p.seed;
+    a.k1 = (uint32_t)(c->p.seed >> 32);
+    a.tick = c->step;
+    sq::Qm1dState st{};
+    st.omega_in = c->omega;
+    st.lrgEl = c->lrgEl;
+    st.lrgVl = c->lrgVl;
+    SQ_HIP(hipMemcpyAsync(c->qst, &st, sizeof st, hipMemcpyHostToDevice, c->qstream));
+    EvPair *e = nullptr;
+    int rc = ev_begin(c, c->qstream, &e);
+    if (rc) return rc;
+    SQ_HIP(sq::qm1d_frame_launch(a, c->qstream));
+    if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
+    SQ_HIP(hipMemcpyAsync(&st, c->qst, sizeof st, hipMemcpyDeviceToHost, c->qstream));
+    SQ_HIP(hipStreamSynchronize(c->qstream));
+    c->step += (unsigned long long)c->p.loops;
+    c->lrgEl = st.lrgEl;
+    c->lrgVl = st.lrgVl;
+    c->perf.steps += st.steps_done;
+    c->perf.site_updates += (long long)st.steps_done * c->N;
+    *stable = st.stable;
+    if (st.stable == 1) {  // tauhost.c:506-532
+        c->qcur ^= 1;
+        c->omega = st.omega_out;
+        c->runs += c->p.loops;
+    }
+    return SQ_OK;
+}
+
+void adapt(sq_ctx *c, int stable) {  // tauhost.c:523-529,537-541
+    if (!c->p.adapt_dtau) return;
+    if (stable == 1) {
+        if (c->stab_cnt > 10) {
+            c->stab_cnt = 0;
+            c->dtau /= 0.950;
+        }
+        c->stab_cnt++;
+    } else {
+        c->dtau *= 0.950;
+        c->stab_cnt = 0;
+    }
+}
+
+int phi4_frame(sq_ctx *c, int *stable) {
+    const size_t plane = plane_floats(c);
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    for (auto &s : c->slabs) {  // frame-start snapshot, kept on device
+        const size_t bytes = (size_t)s.nz * plane * sizeof(float);
+        if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
+        SQ_HIP(hipMemcpyAsync(s.snap, s.buf[c->cur] + plane, bytes, hipMemcpyDeviceToDevice, s.sA));
+    }
+    SQ_HIP(hipMemsetAsync(c->flag, 0, sizeof(int), c->slabs[0].sA));
+    rc = phi4_join(c);
+    if (rc) return rc;
+    for (int j = 0; j < c->p.loops; ++j) {
+        rc = phi4_one_step(c);
+        if (rc) return rc;
+    }
+    rc = phi4_join(c);
+    if (rc) return rc;
+    Slab &s0 = c->slabs[0];
+    if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1) {
+        SQ_NCCL(ncclAllReduce(c->flag, c->flag, 1, ncclInt32, ncclMax, c->comm, s0.sA));
+    }
+    int h = 0;
+    SQ_HIP(hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, s0.sA));
+    SQ_HIP(hipStreamSynchronize(s0.sA));
+    *stable = h ? 0 : 1;
+    if (!*stable) {  // rollback from the device snapshot; the noise counter is NOT rewound,
+                     // so a retried frame draws fresh noise (as the reference's LCG state)
+        for (auto &s : c->slabs)
+            SQ_HIP(hipMemcpyAsync(s.buf[c->cur] + plane, s.snap, (size_t)s.nz * plane * sizeof(float),
+                                  hipMemcpyDeviceToDevice, s.sA));
+        rc = phi4_join(c);
+        if (rc) return rc;
+    }
+    return SQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+void sq_params_init(sq_params *p) {
+    memset(p, 0, sizeof *p);
+    p->struct_size = (int)sizeof(sq_params);
+    p->model = SQ_MODEL_QM1D;
+    p->dims[0] = 200;
+    p->dims[1] = 1;
+    p->dims[2] = 1;
+    p->deltat = 0.02;
+    p->deltatau = 0.002;
+    p->pot = 3;
+    p->C = 1.0;
+    p->loops = 1000;
+    p->seed = 0x5EEDull;
+    p->m2 = 1.0;
+    p->lambda = 1.0;
+    p->clamp = 1000.0;
+    p->device = 0;
+    p->adapt_dtau = 1;
+    p->comm = SQ_COMM_NONE;
+    p->nranks = 1;
+    p->rank = 0;
+    p->nslabs = 1;
+}
+
+const char *sq_last_error(void) { return g_err.c_str(); }
+int sq_abi_version(void) { return SQ_ABI_VERSION; }
+
+int sq_device_count(int *n) {
+    int k = 0;
+    hipError_t e = hipGetDeviceCount(&k);
+    if (e != hipSuccess) k = 0;
+    *n = k;
+    return SQ_OK;
+}
+
+int sq_create(const sq_params *p, sq_ctx **out) {
+    if (!p || !out) return fail(SQ_E_ARG, "null argument");
+    *out = nullptr;
+    if (p->struct_size != (int)sizeof(sq_params)) return fail(SQ_E_ARG, "sq_params size mismatch");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    if (p->device < 0 || p->device >= ndev) return fail(SQ_E_ARG, "device ordinal out of range");
+    if (!(p->deltatau > 0)) return fail(SQ_E_ARG, "deltatau must be > 0");
+    DeviceGuard g(p->device);
+    sq_ctx *c = new sq_ctx();
+    c->p = *p;
+    c->dev = p->device;
+    c->dtau = p->deltatau;
+    int rc = p->model == SQ_MODEL_PHI4 ? create_phi4(c) : p->model == SQ_MODEL_QM1D ? create_qm1d(c)
+                                                                                      : fail(SQ_E_ARG, "unknown model");
+    if (rc) {
+        std::string msg = g_err;
+        sq_destroy(c);
+        g_err = msg;
+        return rc;
+    }
+    *out = c;
+    return SQ_OK;
+}
+
+int sq_destroy(sq_ctx *c) {
+    if (!c) return SQ_OK;
+    DeviceGuard g(c->dev);
+    for (auto &s : c->slabs) {
+        if (s.sA) (void)hipStreamSynchronize(s.sA);
+        if (s.sB) (void)hipStreamSynchronize(s.sB);
+    }
+    if (c->comm) (void)ncclCommDestroy(c->comm);
+    for (auto &s : c->slabs) {
+        (void)hipFree(s.buf[0]);
+        (void)hipFree(s.buf[1]);
+        (void)hipFree(s.snap);
+        if (s.sA) (void)hipStreamDestroy(s.sA);
+        if (s.sB) (void)hipStreamDestroy(s.sB);
+        if (s.evA) (void)hipEventDestroy(s.evA);
+        if (s.evB) (void)hipEventDestroy(s.evB);
+        if (s.evPush) (void)hipEventDestroy(s.evPush);
+    }
+    for (int k = 0; k < 2; ++k) {
+        (void)hipFree(c->qf[k]);
+        (void)hipFree(c->qx[k]);
+        (void)hipFree(c->qxx0[k]);
+    }
+    (void)hipFree(c->qst);
+    (void)hipFree(c->flag);
+    (void)hipFree(c->dacc);
+    (void)hipFree(c->dmax);
+    if (c->qstream) (void)hipStreamDestroy(c->qstream);
+    for (auto &e : c->evpool) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    delete c;
+    return SQ_OK;
+}
+
+int sq_upload(sq_ctx *c, const double *f, const double *x, const double *xx0, double omega, long runs) {
+    if (!c || !f || !x || !xx0) return fail(SQ_E_ARG, "null argument");
+    if (is_phi4(c)) return fail(SQ_E_STATE, "sq_upload is for QM1D contexts");
+    DeviceGuard g(c->dev);
+    const size_t bytes = sizeof(double) * (size_t)c->N;
+    SQ_HIP(hipMemcpy(c->qf[c->qcur], f, bytes, hipMemcpyHostToDevice));
+    SQ_HIP(hipMemcpy(c->qx[c->qcur], x, bytes, hipMemcpyHostToDevice));
+    SQ_HIP(hipMemcpy(c->qxx0[c->qcur], xx0, bytes, hipMemcpyHostToDevice));
+    c->omega = omega;
+    c->runs = runs;
+    return SQ_OK;
+}
+
+int sq_download(sq_ctx *c, double *f, double *x, double *xx0, double *omega, long *runs) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (is_phi4(c)) return fail(SQ_E_STATE, "sq_download is for QM1D contexts");
+    DeviceGuard g(c->dev);
+    const size_t bytes = sizeof(double) * (size_t)c->N;
+    if (f) SQ_HIP(hipMemcpy(f, c->qf[c->qcur], bytes, hipMemcpyDeviceToHost));
+    if (x) SQ_HIP(hipMemcpy(x, c->qx[c->qcur], bytes, hipMemcpyDeviceToHost));
+    if (xx0) SQ_HIP(hipMemcpy(xx0, c->qxx0[c->qcur], bytes, hipMemcpyDeviceToHost));
+    if (omega) *omega = c->omega;
+    if (runs) *runs = c->runs;
+    return SQ_OK;
+}
+
+int sq_qm1d_get_scan(sq_ctx *c, int *lrgEl, double *lrgVl, unsigned long long *tick) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (lrgEl) *lrgEl = c->lrgEl;
+    if (lrgVl) *lrgVl = c->lrgVl;
+    if (tick) *tick = c->step;
+    return SQ_OK;
+}
+
+int sq_qm1d_set_scan(sq_ctx *c, int lrgEl, double lrgVl, unsigned long long tick) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (is_phi4(c)) return fail(SQ_E_STATE, "QM1D only");
+    if (lrgEl < 0 || lrgEl >= c->N) return fail(SQ_E_ARG, "lrgEl out of range");
+    c->lrgEl = lrgEl;
+    c->lrgVl = lrgVl;
+    c->step = tick;
+    return SQ_OK;
+}
+
+int sq_run_frame(sq_ctx *c, int *stable) {
+    if (!c || !stable) return fail(SQ_E_ARG, "null argument");
+    DeviceGuard g(c->dev);
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = is_phi4(c) ? phi4_frame(c, stable) : qm1d_frame(c, stable);
+    if (rc) return rc;
+    adapt(c, *stable);
+    c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SQ_OK;
+}
+
+int sq_step(sq_ctx *c, int nsteps) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "sq_step is for PHI4 contexts (QM1D uses sq_run_frame)");
+    if (nsteps < 0) return fail(SQ_E_ARG, "nsteps < 0");
+    DeviceGuard g(c->dev);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < nsteps; ++i) {
+        int rc = phi4_one_step(c);
+        if (rc) return rc;
+    }
+    c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SQ_OK;
+}
+
+int sq_sync(sq_ctx *c) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    DeviceGuard g(c->dev);
+    if (c->qstream) SQ_HIP(hipStreamSynchronize(c->qstream));
+    return phi4_join(c);
+}
+
+int sq_slab(sq_ctx *c, long long *nz_local, long long *z0) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    long long n = 0;
+    for (auto &s : c->slabs) n += s.nz;
+    if (nz_local) *nz_local = n;
+    if (z0) *z0 = c->slabs[0].z0;
+    return SQ_OK;
+}
+
+int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {
+    if (!c || !phi) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    DeviceGuard g(c->dev);
+    const size_t plane = plane_floats(c);
+    size_t need = 0;
+    for (auto &s : c->slabs) need += (size_t)s.nz * plane;
+    if (count != need) return fail(SQ_E_ARG, "field size mismatch");
+    SQ_HIP(hipDeviceSynchronize());
+    size_t off = 0;
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipMemcpy(s.buf[c->cur] + plane, phi + off, (size_t)s.nz * plane * sizeof(float),
+                         hipMemcpyHostToDevice));
+        off += (size_t)s.nz * plane;
+    }
+    return SQ_OK;
+}
+
+int sq_download_field(sq_ctx *c, float *phi, size_t count) {
+    if (!c || !phi) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    DeviceGuard g(c->dev);
+    const size_t plane = plane_floats(c);
+    size_t need = 0;
+    for (auto &s : c->slabs) need += (size_t)s.nz * plane;
+    if (count != need) return fail(SQ_E_ARG, "field size mismatch");
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    size_t off = 0;
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipMemcpy(phi + off, s.buf[c->cur] + plane, (size_t)s.nz * plane * sizeof(float),
+                         hipMemcpyDeviceToHost));
+        off += (size_t)s.nz * plane;
+    }
+    return SQ_OK;
+}
+
+int sq_init_field(sq_ctx *c, float amp) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    DeviceGuard g(c->dev);
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    for (auto &s : c->slabs)
+        SQ_HIP(sq::phi4_init_launch(s.buf[c->cur], c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
+                                    (uint32_t)(c->p.seed >> 32), amp, s.sA));
+    return phi4_join(c);
+}
+
+int sq_moments(sq_ctx *c, double out[3]) {
+    if (!c || !out) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    DeviceGuard g(c->dev);
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    const size_t plane = plane_floats(c);
+    out[0] = out[1] = out[2] = 0;
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipMemset(c->dacc, 0, 2 * sizeof(double)));
+        SQ_HIP(hipMemset(c->dmax, 0, sizeof(unsigned int)));
+        SQ_HIP(sq::phi4_moments_launch(s.buf[c->cur] + plane, (long long)s.nz * (long long)plane,
+                                       c->dacc, c->dmax, s.sA));
+        double acc[2];
+        unsigned int mx;
+        SQ_HIP(hipStreamSynchronize(s.sA));
+        SQ_HIP(hipMemcpy(acc, c->dacc, sizeof acc, hipMemcpyDeviceToHost));
+        SQ_HIP(hipMemcpy(&mx, c->dmax, sizeof mx, hipMemcpyDeviceToHost));
+        float fm;
+        memcpy(&fm, &mx, sizeof fm);
+        out[0] += acc[0];
+        out[1] += acc[1];
+        out[2] = std::max(out[2], (double)fm);
+    }
+    return SQ_OK;
+}
+
+int sq_set_dtau(sq_ctx *c, double dtau) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!(dtau > 0)) return fail(SQ_E_ARG, "dtau must be > 0");
+    c->dtau = dtau;
+    return SQ_OK;
+}
+int sq_get_dtau(sq_ctx *c, double *dtau) {
+    if (!c || !dtau) return fail(SQ_E_ARG, "null argument");
+    *dtau = c->dtau;
+    return SQ_OK;
+}
+int sq_get_step(sq_ctx *c, unsigned long long *step) {
+    if (!c || !step) return fail(SQ_E_ARG, "null argument");
+    *step = c->step;
+    return SQ_OK;
+}
+int sq_set_step(sq_ctx *c, unsigned long long step) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    c->step = step;
+    return SQ_OK;
+}
+
+int sq_correlator(sq_ctx *c, double *out, int n) {
+    if (!c || !out || n < 0) return fail(SQ_E_ARG, "bad argument");
+    DeviceGuard g(c->dev);
+    if (!is_phi4(c)) {
+        if (n > c->N) return fail(SQ_E_ARG, "n > N");
+        std::vector<double> x(c->N), xx0(c->N);
+        int rc = sq_download(c, nullptr, x.data(), xx0.data(), nullptr, nullptr);
+        if (rc) return rc;
+        const int mid = c->N / 2;
+        for (int i = 0; i < n; ++i) out[i] = xx0[i] - x[i] * x[mid];  // tauhost.c:519-521
+        return SQ_OK;
+    }
+    if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1)
+        return fail(SQ_E_STATE, "slice correlator needs the whole lattice in this process");
+    if (n > c->Lz) return fail(SQ_E_ARG, "n > Lz");
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    std::vector<double> S;
+    double *d = nullptr;
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipMalloc(&d, sizeof(double) * s.nz));
+        hipError_t e = sq::phi4_slices_launch(s.buf[c->cur], c->Lx, c->Ly, s.nz, d, s.sA);
+        std::vector<double> h(s.nz);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
+        if (e == hipSuccess) e = hipMemcpy(h.data(), d, sizeof(double) * s.nz, hipMemcpyDeviceToHost);
+        (void)hipFree(d);
+        if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+        S.insert(S.end(), h.begin(), h.end());
+    }
+    const long long Lz = c->Lz;
+    const double vol = (double)c->Lx * c->Ly * (double)Lz;
+    for (int t = 0; t < n; ++t) {
+        double acc = 0;
+        for (long long z = 0; z < Lz; ++z) acc += S[z] * S[(z + t) % Lz];
+        out[t] = acc / vol;
+    }
+    return SQ_OK;
+}
+
+int sq_set_profiling(sq_ctx *c, int on) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    c->profiling = on != 0;
+    return SQ_OK;
+}
+
+int sq_perf(sq_ctx *c, sq_perf_t *out) {
+    if (!c || !out) return fail(SQ_E_ARG, "null argument");
+    DeviceGuard g(c->dev);
+    int rc = flush_events(c);
+    if (rc) return rc;
+    *out = c->perf;
+    return SQ_OK;
+}
+
+int sq_perf_reset(sq_ctx *c) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    DeviceGuard g(c->dev);
+    int rc = flush_events(c);
+    if (rc) return rc;
+    c->perf = sq_perf_t{};
+    return SQ_OK;
+}
+
+int sq_comm_unique_id(unsigned char out[128]) {
+    if (!out) return fail(SQ_E_ARG, "null argument");
+    ncclUniqueId id;
+    SQ_NCCL(ncclGetUniqueId(&id));
+    memset(out, 0, 128);
+    memcpy(out, id.internal, sizeof(id.internal));
+    return SQ_OK;
+}
+
+int sq_selftest_normals(int device, unsigned long long seed, unsigned int stream,
+                        unsigned long long quad0, unsigned long long step, float *out, size_t nquads) {
+    if (!out) return fail(SQ_E_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    float *d = nullptr;
+    SQ_HIP(hipMalloc(&d, nquads * 4 * sizeof(float)));
+    hipError_t e = sq::selftest_normals_launch(d, nquads, quad0, stream, step, (uint32_t)seed,
+                                               (uint32_t)(seed >> 32), nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d, nquads * 4 * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
+int sq_selftest_dpp(int device, float *out64x2) {
+    if (!out64x2) return fail(SQ_E_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    float *d = nullptr;
+    SQ_HIP(hipMalloc(&d, 128 * sizeof(float)));
+    hipError_t e = sq::selftest_dpp_launch(d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out64x2, d, 128 * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
+int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int key[2],
+                       unsigned int out[4]) {
+    if (!ctr || !key || !out) return fail(SQ_E_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    uint32_t h[6] = {ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1]};
+    uint32_t *d = nullptr;
+    SQ_HIP(hipMalloc(&d, 10 * sizeof(uint32_t)));
+    hipError_t e = hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = sq::selftest_philox_launch(d, d + 6, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d + 6, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
+int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps) {
+    if (!gbps || iters < 1 || bytes < 1024) return fail(SQ_E_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    const size_t n4 = bytes / 16;
+    float4 *a = nullptr, *b = nullptr;
+    SQ_HIP(hipMalloc(&a, n4 * 16));
+    SQ_HIP(hipMalloc(&b, n4 * 16));
+    SQ_HIP(hipMemset(a, 0, n4 * 16));
+    hipEvent_t e0, e1;
+    SQ_HIP(hipEventCreate(&e0));
+    SQ_HIP(hipEventCreate(&e1));
+    SQ_HIP(sq::copy_launch(a, b, n4, nullptr));
+    SQ_HIP(hipEventRecord(e0, nullptr));
+    for (int i = 0; i < iters; ++i) SQ_HIP(sq::copy_launch((i & 1) ? b : a, (i & 1) ? a : b, n4, nullptr));
+    SQ_HIP(hipEventRecord(e1, nullptr));
+    SQ_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    SQ_HIP(hipEventElapsedTime(&ms, e0, e1));
+    *gbps = 2.0 * (double)n4 * 16.0 * iters / (ms * 1e-3) / 1e9;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(a);
+    (void)hipFree(b);
+    return SQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+// sq_internal.h -- kernel argument blocks and launchers shared between the
+// kernel translation units and the C-ABI layer (sq_api.cpp).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sq {
+
+// ---------------------------------------------------------------- PHI4 ----
+// One slab lives in a padded buffer of (nz + 2) planes of Lx*Ly floats, z
+// slowest: padded plane 0 is the lower ghost (global z0-1), planes 1..nz the
+// slab, plane nz+1 the upper ghost.  With periodic != 0 the slab is the whole
+// lattice in z and the kernel wraps z itself (ghosts unused).
+struct Phi4StepArgs {
+    const float *in;
+    float *out;
+    int Lx, Ly, nz;
+    int zlo, zhi, zstep, zc, nzc;  // chunk k updates planes [zlo + k*zstep, +zc) clipped to zhi
+    int periodic;
+    int nxseg, nyg, nunits;
+    long long zg0;            // global z of local plane 0
+    float h, m2, lam6, sig, clampv;
+    uint32_t k0, k1, s_lo, s_hi;
+    int *flag;                // guard flag: set to 1 when a site was clamped / NaN (nullable)
+};
+
+struct Phi4Geom {
+    int qx;   // lanes per x segment (4 sites each)
+    int r;    // rows per lane
+    int wy;   // rows per wave unit
+};
+
+// Picks the register tile for (Lx, Ly); returns false if unsupported.
+bool phi4_geometry(int Lx, int Ly, Phi4Geom *g);
+// Fills the work decomposition of a launch that updates `nzc` chunks.
+void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g);
+hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s);
+hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
+                            uint32_t k1, float amp, hipStream_t s);
+// Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2, acc[2] = max |phi| (as
+// ordered-int bits in acc_max).  acc must be zeroed by the caller.
+hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max,
+                               hipStream_t s);
+// Slice sums S(z) = sum_{x,y} phi(x,y,z) for z in [0,nz): out[z] (double).
+hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double *out,
+                              hipStream_t s);
+
+// ---------------------------------------------------------------- QM1D ----
+struct Qm1dState {    // device-resident frame scalars
+    double omega_in;  // ω at frame start
+    double omega_out; // ω after the frame
+    double lrgVl;     // carried running max |X| (tauhost.c:66, never rolled back)
+    int lrgEl;        // carried leader index (tauhost.c:65)
+    int stable;       // 1 stable, 0 unstable
+    int steps_done;
+    int pad;
+};
+
+struct Qm1dArgs {
+    const double *f, *x, *xx0;  // frame-start state (N)
+    double *nf, *nx, *nxx0;     // state after the frame (N)
+    Qm1dState *st;
+    int N, pot, loops, runs;
+    double a, a2, h, sig, sigw, kconst;
+    uint32_t k0, k1;
+    unsigned long long tick;    // Philox step index of the frame's first step
+};
+
+int qm1d_sites_per_thread(int N);  // 0 if N unsupported
+hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
+
+// -------------------------------------------------------------- selftest --
+hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long quad0,
+                                   uint32_t stream, unsigned long long step, uint32_t k0,
+                                   uint32_t k1, hipStream_t s);
+hipError_t selftest_dpp_launch(float *out, hipStream_t s);
+hipError_t selftest_philox_launch(const uint32_t *ck, uint32_t *out, hipStream_t s);
+hipError_t copy_launch(const float4 *in, float4 *out, size_t n4, hipStream_t s);
+
+}  // namespace sq

@@ -1,0 +1,252 @@
+// sq_qm1d.hip -- the reference model (tau_kernel.cl:25-175) on gfx950, fp64.
+//
+// One frame = `loops` Euler-Maruyama steps of the fluctuation chain f (N sites,
+// Dirichlet ghosts) plus the collective coordinate omega, in ONE launch of ONE
+// workgroup (the reference also relies on a single work-group: its barrier at
+// tau_kernel.cl:168 is the only step-to-step sync).  What differs by design:
+//   * Jacobi ordering: every site reads the old field (the reference's order
+//     is whatever its runtime serialises);
+//   * noise from Philox4x32-10 per (site, step) instead of one shared LCG
+//     that every work-item races on (tau_kernel.cl:269-284);
+//   * the stability scan (tau_kernel.cl:135-143, racy shared lrgEl/lrgVl)
+//     becomes an order-independent block prefix-max scan with the serial
+//     scan's meaning (oracle/orc_qm1d.c, orc_qm1d_frame);
+//   * omega is computed redundantly by every thread from its own counter-based
+//     normal, so no broadcast is needed.
+// Thread t owns K consecutive sites in registers; neighbour edges, f[mid] and
+// scan partials go through LDS.  Expressions keep the reference's order and
+// the file is built with -ffp-contract=off, so for potID 0 the deterministic
+// part is bit-identical to the oracle.
+#include "sq_internal.h"
+#include "sq_rng.h"
+
+namespace sq {
+
+namespace {
+
+constexpr double kEta = .8;  // tau_kernel.cl:19-22
+constexpr double kV0 = 2.;
+constexpr double kM = 1.;
+constexpr int kMaxThreads = 1024;
+
+__device__ __forceinline__ double xcl(double t, double w, int pot) {  // clas(), :184-189,215-226
+    if (pot == 3) {
+        const double s = 2.0;  // (double)sqrtf((float)(2.*V0/m)) == 2 exactly
+        return kEta * (double)tanhf((float)(s * (t - w) / kEta));
+    }
+    return 0.;
+}
+__device__ __forceinline__ double ddpot(double x, int pot) {  // ddPot(), :190-195,227-236
+    if (pot == 3) return (12. * kV0 * x * x / (kEta * kEta) - 4. * kV0) / (kEta * kEta);
+    return 2.;
+}
+__device__ __forceinline__ double absol(double v) { return v <= 0 ? -v : v; }
+
+__device__ __forceinline__ double wave_incl_max(double v, int lane) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(v, o, 64);
+        if (lane >= o) v = fmax(v, u);
+    }
+    return v;
+}
+
+template <int K>
+__global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs A) {
+    __shared__ double s_first[kMaxThreads], s_last[kMaxThreads];
+    __shared__ double s_wmaxX[kMaxThreads / 64], s_wmaxA[kMaxThreads / 64];
+    __shared__ double s_fmid, s_R;
+    __shared__ int s_leader[2];
+
+    const int N = A.N, pot = A.pot, mid = N / 2;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
+    const int i0 = t * K;
+    const double h = A.h, a = A.a, a2 = A.a2;
+
+    double f[K], x[K], xx0[K], Xn[K], dchk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = i0 + k;
+        f[k] = i < N ? A.f[i] : 0.;
+        x[k] = i < N ? A.x[i] : 0.;
+        xx0[k] = i < N ? A.xx0[i] : 0.;
+    }
+    double om = A.st->omega_in;
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int stable = 1, steps = 0;
+
+    for (int j = 0; j < A.loops; ++j) {
+        const unsigned long long step = A.tick + (unsigned long long)j;
+        const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
+        // ---- phase 1: publish edges and f[mid] (old field) ----
+        s_first[t] = f[0];
+        s_last[t] = f[K - 1];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (i0 + k == mid) s_fmid = f[k];
+        if (t == 0) s_leader[j & 1] = -1;
+        __syncthreads();
+        const double fL = t > 0 ? s_last[t - 1] : 0.;
+        const double fR = (t + 1 < (int)blockDim.x) ? s_first[t + 1] : 0.;
+        const double fmid = s_fmid;
+        const double Xm = fmid + xcl((double)mid * a, om, pot);
+        const double den = (double)(A.runs + j + 1);
+
+        // ---- phase 2: site updates ----
+        float nz[K < 4 ? 4 : K];
+        if constexpr (K >= 4) {
+#pragma unroll
+            for (int q = 0; q < K / 4; ++q) {
+                const f32x4n n = normals4((unsigned long long)((i0 >> 2) + q), kStreamField, slo, shi,
+                                          A.k0, A.k1);
+                nz[4 * q] = n.a;
+                nz[4 * q + 1] = n.b;
+                nz[4 * q + 2] = n.c;
+                nz[4 * q + 3] = n.d;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = i0 + k;
+                const f32x4n n = normals4((unsigned long long)(i >> 2), kStreamField, slo, shi, A.k0,
+                                          A.k1);
+                const int c = i & 3;
+                nz[k] = c == 0 ? n.a : c == 1 ? n.b : c == 2 ? n.c : n.d;
+            }
+        }
+        double prev_old = fL;  // old f[i-1]
+        double lmaxX = -INFINITY, lmaxA = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = i0 + k;
+            if (i >= N) break;
+            const double fi = f[k];
+            const double xc = xcl((double)i * a, om, pot);
+            const double dw = A.sig * (double)nz[k];
+            const double fr = (k + 1 < K) ? f[k + 1] : fR;
+            double v;
+            if (i == 0)
+                v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
+                    ddpot(xc, pot) * fi * h + dw;
+            else if (i == N - 1)
+                v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
+                    ddpot(xc, pot) * fi * h + dw;
+            else
+                v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
+            if (v > 1000) v = 1000;  // guard, :119-133
+            if (v < -1000) v = -1000;
+            if (v != v) v = 1000;
+            dchk[k] = absol(v - fi - dw);
+            const double X = v + xc;
+            Xn[k] = X;
+            lmaxX = fmax(lmaxX, X);
+            lmaxA = fmax(lmaxA, absol(X));
+            // running means from the OLD field, :144-145
+            const double Xi = fi + xc;
+            xx0[k] = xx0[k] + (Xi * Xm - xx0[k]) / den;
+            x[k] = x[k] + (Xi - x[k]) / den;
+            prev_old = fi;
+            f[k] = v;
+        }
+        if (E >= i0 && E < i0 + K) {
+#pragma unroll
+            for (int k = 0; k < K; ++k)
+                if (i0 + k == E) s_R = Xn[k];
+        }
+        // ---- phase 3: block exclusive prefix max of X' and |X'| ----
+        const double ix = wave_incl_max(lmaxX, lane);
+        const double ia = wave_incl_max(lmaxA, lane);
+        double ex = __shfl_up(ix, 1, 64), ea = __shfl_up(ia, 1, 64);
+        if (lane == 0) {
+            ex = -INFINITY;
+            ea = -INFINITY;
+        }
+        if (lane == 63) {
+            s_wmaxX[wv] = ix;
+            s_wmaxA[wv] = ia;
+        }
+        __syncthreads();
+        double runX = s_R, runA = V, totA = V;
+        for (int w = 0; w < nw; ++w) {
+            const double wx = s_wmaxX[w], wa = s_wmaxA[w];
+            if (w < wv) {
+                runX = fmax(runX, wx);
+                runA = fmax(runA, wa);
+            }
+            totA = fmax(totA, wa);
+        }
+        runX = fmax(runX, ex);
+        runA = fmax(runA, ea);
+        int unst = 0, leader = -1;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            const int i = i0 + k;
+            if (i >= N) break;
+            if (Xn[k] > runX) {
+                runX = Xn[k];
+                leader = i;
+                if (dchk[k] > runA) unst = 1;
+            }
+            runA = fmax(runA, absol(Xn[k]));
+        }
+        if (leader >= 0) atomicMax(&s_leader[j & 1], leader);
+        const int any_unst = __syncthreads_or(unst);
+        const int L = s_leader[j & 1];
+        if (L >= 0) E = L;
+        V = totA;
+        // ---- collective coordinate, :103-110,155-167 (uniform) ----
+        const f32x4n nwn = normals4(0ull, kStreamOmega, slo, shi, A.k0, A.k1);
+        const double nwo = om + A.kconst * (A.sigw * (double)nwn.a);
+        const double top = (double)(N - 1) * a;
+        if (nwo > top) om = 2 * (double)(N - 1) * a - nwo;
+        else if (nwo < 0) om = -nwo;
+        else om = nwo;
+        steps = j + 1;
+        if (any_unst) {
+            stable = 0;
+            break;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = i0 + k;
+        if (i < N) {
+            A.nf[i] = f[k];
+            A.nx[i] = x[k];
+            A.nxx0[i] = xx0[k];
+        }
+    }
+    if (t == 0) {
+        A.st->omega_out = om;
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = stable;
+        A.st->steps_done = steps;
+    }
+}
+
+}  // namespace
+
+int qm1d_sites_per_thread(int N) {
+    if (N < 2) return 0;
+    for (int k : {1, 2, 4, 8})
+        if ((N + k - 1) / k <= kMaxThreads) return k;
+    return 0;
+}
+
+hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
+    const int K = qm1d_sites_per_thread(a.N);
+    if (K == 0) return hipErrorInvalidValue;
+    int threads = (a.N + K - 1) / K;
+    threads = ((threads + 63) / 64) * 64;
+    switch (K) {
+    case 1: hipLaunchKernelGGL(qm1d_frame_kernel<1>, dim3(1), dim3(threads), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(qm1d_frame_kernel<2>, dim3(1), dim3(threads), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(qm1d_frame_kernel<4>, dim3(1), dim3(threads), 0, s, a); break;
+    default: hipLaunchKernelGGL(qm1d_frame_kernel<8>, dim3(1), dim3(threads), 0, s, a); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace sq

@@ -1,0 +1,75 @@
+// sq_selftest.hip -- small device kernels used by tests and bench.py: the
+// Philox/Box-Muller normals exactly as the step kernels draw them (for the
+// RNG parity test), a DPP lane-rotation probe (the x-neighbour exchange of the
+// phi^4 kernel relies on wave_ror/wave_rol semantics), and a float4 streaming
+// copy that measures the attainable HBM rate on the box.
+#include "sq_internal.h"
+#include "sq_rng.h"
+
+namespace sq {
+
+namespace {
+
+__global__ __launch_bounds__(256) void normals_kernel(float *out, size_t nquads,
+                                                     unsigned long long quad0, uint32_t stream,
+                                                     unsigned long long step, uint32_t k0,
+                                                     uint32_t k1) {
+    const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nquads) return;
+    const f32x4n n = normals4(quad0 + q, stream, (uint32_t)step, (uint32_t)(step >> 32), k0, k1);
+    out[4 * q] = n.a;
+    out[4 * q + 1] = n.b;
+    out[4 * q + 2] = n.c;
+    out[4 * q + 3] = n.d;
+}
+
+__global__ void dpp_kernel(float *out) {
+    const int lane = threadIdx.x & 63;
+    const int v = lane;
+    out[lane] = (float)__builtin_amdgcn_update_dpp(0, v, 0x13C, 0xF, 0xF, false);       // wave_ror:1
+    out[64 + lane] = (float)__builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, false);  // wave_rol:1
+}
+
+__global__ void philox_kernel(const uint32_t *ck, uint32_t *out) {
+    const u32x4 o = philox4x32_10(u32x4{ck[0], ck[1], ck[2], ck[3]}, ck[4], ck[5]);
+    out[0] = o.x;
+    out[1] = o.y;
+    out[2] = o.z;
+    out[3] = o.w;
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in,
+                                                   float4 *__restrict__ out, size_t n4) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (size_t)gridDim.x * blockDim.x)
+        out[i] = in[i];
+}
+
+}  // namespace
+
+hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long quad0,
+                                   uint32_t stream, unsigned long long step, uint32_t k0,
+                                   uint32_t k1, hipStream_t s) {
+    const unsigned grid = (unsigned)((nquads + 255) / 256);
+    hipLaunchKernelGGL(normals_kernel, dim3(grid), dim3(256), 0, s, out, nquads, quad0, stream, step,
+                       k0, k1);
+    return hipGetLastError();
+}
+
+hipError_t selftest_dpp_launch(float *out, hipStream_t s) {
+    hipLaunchKernelGGL(dpp_kernel, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
+
+hipError_t selftest_philox_launch(const uint32_t *ck, uint32_t *out, hipStream_t s) {
+    hipLaunchKernelGGL(philox_kernel, dim3(1), dim3(1), 0, s, ck, out);
+    return hipGetLastError();
+}
+
+hipError_t copy_launch(const float4 *in, float4 *out, size_t n4, hipStream_t s) {
+    const unsigned grid = (unsigned)std::min<size_t>((n4 + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, s, in, out, n4);
+    return hipGetLastError();
+}
+
+}  // namespace sq

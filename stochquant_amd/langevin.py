@@ -1,0 +1,255 @@
+"""Host-side mirror of the reference's interface for the Langevin path.
+
+The reference exposes no Python API: `taumain.py:132` spawns `./tauhost.o`
+with 13 positional arguments and parses its stdout.  This module offers that
+same contract (`run_tauhost`, `parse_frame_line`) plus thin numpy wrappers of
+the C ABI for the two models:
+
+* `Qm1dChain`  -- tau_kernel.cl time_dev + the tauhost.c frame loop (fp64)
+* `Phi4Lattice` -- the 3-D fp32 north-star extension (slab / multi-GPU)
+
+Everything computes on the MI355X through libstochquant.so; nothing here has a
+CPU path.
+"""
+import ctypes
+import io
+import os
+import subprocess
+
+import numpy as np
+
+from . import _lib
+from ._lib import SQ_COMM_LOOPBACK, SQ_COMM_NONE, SQ_COMM_RCCL, SQ_MODEL_PHI4, SQ_MODEL_QM1D
+
+_DP = ctypes.POINTER(ctypes.c_double)
+_FP = ctypes.POINTER(ctypes.c_float)
+
+
+def _dptr(a):
+    return a.ctypes.data_as(_DP)
+
+
+def _fptr(a):
+    return a.ctypes.data_as(_FP)
+
+
+class _Ctx:
+    def __init__(self, params):
+        self._h = ctypes.c_void_p()
+        _lib.call("sq_create", ctypes.byref(params), ctypes.byref(self._h))
+        self.params = params
+
+    def close(self):
+        if self._h:
+            _lib.call("sq_destroy", self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # shared controls ------------------------------------------------------
+    @property
+    def dtau(self):
+        d = ctypes.c_double()
+        _lib.call("sq_get_dtau", self._h, ctypes.byref(d))
+        return d.value
+
+    @dtau.setter
+    def dtau(self, v):
+        _lib.call("sq_set_dtau", self._h, float(v))
+
+    @property
+    def step_counter(self):
+        s = ctypes.c_ulonglong()
+        _lib.call("sq_get_step", self._h, ctypes.byref(s))
+        return s.value
+
+    @step_counter.setter
+    def step_counter(self, v):
+        _lib.call("sq_set_step", self._h, int(v))
+
+    def run_frame(self):
+        """`loops` steps + stability check + rollback + Δτ control; returns True if stable."""
+        st = ctypes.c_int()
+        _lib.call("sq_run_frame", self._h, ctypes.byref(st))
+        return st.value == 1
+
+    def set_profiling(self, on=True):
+        _lib.call("sq_set_profiling", self._h, 1 if on else 0)
+
+    def perf(self):
+        p = _lib.SqPerf()
+        _lib.call("sq_perf", self._h, ctypes.byref(p))
+        return {k: getattr(p, k) for k, _ in p._fields_}
+
+    def perf_reset(self):
+        _lib.call("sq_perf_reset", self._h)
+
+    def sync(self):
+        _lib.call("sq_sync", self._h)
+
+
+class Qm1dChain(_Ctx):
+    """The reference's 1-D chain: N sites (Δt spacing), potID 0 or 3, noise C,
+    `loops` steps per frame (tauhost.c argv[1..10] meaning)."""
+
+    def __init__(self, N, deltat, deltatau, pot=3, C=1.0, loops=1000, seed=0x5EED, device=0,
+                 adapt_dtau=True):
+        p = _lib.default_params()
+        p.model = SQ_MODEL_QM1D
+        p.dims[0] = int(N)
+        p.deltat = float(deltat)
+        p.deltatau = float(deltatau)
+        p.pot = int(pot)
+        p.C = float(C)
+        p.loops = int(loops)
+        p.seed = int(seed)
+        p.device = int(device)
+        p.adapt_dtau = 1 if adapt_dtau else 0
+        super().__init__(p)
+        self.N = int(N)
+
+    def upload(self, f, x=None, xx0=None, omega=0.0, runs=0):
+        f = np.ascontiguousarray(f, dtype=np.float64)
+        x = np.zeros(self.N) if x is None else np.ascontiguousarray(x, dtype=np.float64)
+        xx0 = np.zeros(self.N) if xx0 is None else np.ascontiguousarray(xx0, dtype=np.float64)
+        if f.shape != (self.N,) or x.shape != (self.N,) or xx0.shape != (self.N,):
+            raise ValueError("state arrays must have N entries")
+        _lib.call("sq_upload", self._h, _dptr(f), _dptr(x), _dptr(xx0), float(omega), int(runs))
+
+    def download(self):
+        f, x, xx0 = np.empty(self.N), np.empty(self.N), np.empty(self.N)
+        om = ctypes.c_double()
+        runs = ctypes.c_long()
+        _lib.call("sq_download", self._h, _dptr(f), _dptr(x), _dptr(xx0), ctypes.byref(om), ctypes.byref(runs))
+        return {"f": f, "x": x, "xx0": xx0, "omega": om.value, "runs": runs.value}
+
+    @property
+    def scan(self):
+        e, v, t = ctypes.c_int(), ctypes.c_double(), ctypes.c_ulonglong()
+        _lib.call("sq_qm1d_get_scan", self._h, ctypes.byref(e), ctypes.byref(v), ctypes.byref(t))
+        return {"lrgEl": e.value, "lrgVl": v.value, "tick": t.value}
+
+    def set_scan(self, lrgEl, lrgVl, tick):
+        _lib.call("sq_qm1d_set_scan", self._h, int(lrgEl), float(lrgVl), int(tick))
+
+    def xavg(self):
+        """xavg = xx0 - x * x[mid] (tauhost.c:519-521)."""
+        out = np.empty(self.N)
+        _lib.call("sq_correlator", self._h, _dptr(out), self.N)
+        return out
+
+
+class Phi4Lattice(_Ctx):
+    """Periodic 3-D φ⁴ lattice (Lx, Ly, Lz) in fp32, V = m²/2 φ² + λ/24 φ⁴.
+
+    comm="none"     one slab, z wraps in-kernel
+    comm="loopback" `nslabs` slabs on one device, halos by D2D copies
+    comm="rccl"     one slab per process (rank / nranks), halos over RCCL;
+                    `comm_id` from `unique_id()` on rank 0
+    """
+
+    def __init__(self, shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, device=0, comm="none",
+                 nslabs=1, nranks=1, rank=0, comm_id=None, clamp=1000.0, loops=100, C=1.0,
+                 adapt_dtau=True):
+        p = _lib.default_params()
+        p.model = SQ_MODEL_PHI4
+        for i in range(3):
+            p.dims[i] = int(shape[i])
+        p.deltatau = float(dtau)
+        p.m2 = float(m2)
+        p.lambda_ = float(lam)
+        p.seed = int(seed)
+        p.device = int(device)
+        p.clamp = float(clamp)
+        p.loops = int(loops)
+        p.C = float(C)
+        p.adapt_dtau = 1 if adapt_dtau else 0
+        p.comm = {"none": SQ_COMM_NONE, "loopback": SQ_COMM_LOOPBACK, "rccl": SQ_COMM_RCCL}[comm]
+        p.nslabs = int(nslabs)
+        p.nranks = int(nranks)
+        p.rank = int(rank)
+        if comm_id is not None:
+            b = bytes(comm_id)
+            ctypes.memmove(p.comm_id, b, min(len(b), 128))
+        super().__init__(p)
+        self.shape = tuple(int(s) for s in shape)
+        nz, z0 = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.call("sq_slab", self._h, ctypes.byref(nz), ctypes.byref(z0))
+        self.nz_local, self.z0 = nz.value, z0.value
+
+    @property
+    def local_shape(self):
+        return (self.nz_local, self.shape[1], self.shape[0])  # numpy order: z, y, x
+
+    def step(self, n=1):
+        _lib.call("sq_step", self._h, int(n))
+
+    def upload(self, phi):
+        a = np.ascontiguousarray(phi, dtype=np.float32)
+        if a.size != int(np.prod(self.local_shape)):
+            raise ValueError(f"field must have {self.local_shape} entries")
+        _lib.call("sq_upload_field", self._h, _fptr(a), a.size)
+
+    def download(self):
+        a = np.empty(self.local_shape, dtype=np.float32)
+        _lib.call("sq_download_field", self._h, _fptr(a), a.size)
+        return a
+
+    def init_field(self, amp):
+        _lib.call("sq_init_field", self._h, float(amp))
+
+    def moments(self):
+        out = np.zeros(3)
+        _lib.call("sq_moments", self._h, _dptr(out))
+        return {"sum": out[0], "sum2": out[1], "maxabs": out[2]}
+
+    def correlator(self, n=None):
+        n = self.shape[2] if n is None else int(n)
+        out = np.empty(n)
+        _lib.call("sq_correlator", self._h, _dptr(out), n)
+        return out
+
+
+def unique_id():
+    """RCCL unique id (128 bytes) for SQ_COMM_RCCL contexts."""
+    buf = (ctypes.c_ubyte * 128)()
+    _lib.call("sq_comm_unique_id", buf)
+    return bytes(buf)
+
+
+# --------------------------------------------------------------------------
+# Process/CLI contract of the reference (taumain.py:132 -> tauhost.o)
+# --------------------------------------------------------------------------
+TAUHOST_ARGS = ("n", "deltat", "deltatau", "frames", "potID", "c", "device", "rpf", "intime",
+                "loops", "inputf", "outputf", "acco")
+
+
+def tauhost_argv(n, deltat, deltatau, frames, potID, c, device, rpf, intime, loops, inputf, outputf,
+                 acco, exe=None):
+    """argv exactly as taumain.py:132 builds it (every value passed through str())."""
+    exe = exe or _lib.TAUHOST_PATH
+    return [exe] + [str(v) for v in (n, deltat, deltatau, frames, potID, c, device, rpf, intime, loops,
+                                     inputf, outputf, acco)]
+
+
+def run_tauhost(argv, cwd=None, timeout=600, env=None):
+    """Run the drop-in executable; returns CompletedProcess with bytes stdout."""
+    if not os.path.exists(argv[0]):
+        raise _lib.StochQuantUnavailable(f"{argv[0]} not built")
+    return subprocess.run(argv, cwd=cwd, capture_output=True, timeout=timeout, env=env)
+
+
+def parse_frame_line(line):
+    """taumain.py:30-41: np.genfromtxt(delimiter='|'); last two fields Δτ, percent."""
+    tmp = np.genfromtxt(io.BytesIO(line.strip()), delimiter="|")
+    return {"y": tmp[:-2], "dtau": tmp[-2], "percent": tmp[-1]}

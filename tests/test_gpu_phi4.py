@@ -1,0 +1,204 @@
+"""3-D φ⁴ hot path on the MI355X vs the oracle.
+
+Parity contract (fp32):
+  * C = 0 (noise off): the GPU step is BIT-IDENTICAL to the oracle -- same
+    fp32 operations in the same order (explicit fma, -ffp-contract=off).
+  * C = 1: the only difference is the hardware transcendentals of the noise;
+    one step differs by at most  sigma*(NORMAL_ATOL + NORMAL_RTOL*|xi|) plus one
+    rounding of phi', i.e.  |d| <= STEP_ATOL + STEP_RTOL*|phi'|  per step, and
+    the update is a contraction for these parameters (row sum of the Jacobian
+    1 - h*V'' < 1), so k steps stay within k times that bound.
+  * Slab decomposition (loopback slabs, RCCL self-exchange) is bit-identical
+    to the monolithic run with the noise on.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+STEP_ATOL = 4e-6
+STEP_RTOL = 2.5e-7
+
+SHAPES = [
+    (8, 8, 8), (16, 16, 16), (32, 32, 32), (32, 8, 13), (64, 16, 8), (128, 16, 9),
+    (256, 8, 8), (256, 4, 33), (512, 4, 4), (768, 2, 5),
+]
+
+
+def _lat(shape, C=1.0, dtau=0.02, m2=0.5, lam=1.0, seed=1234, **kw):
+    from stochquant_amd import Phi4Lattice
+    return Phi4Lattice(shape, dtau=dtau, m2=m2, lam=lam, seed=seed, C=C, **kw)
+
+
+def _oracle_run(oracle_mod, shape, phi, steps, C=1.0, dtau=0.02, m2=0.5, lam=1.0, seed=1234, step0=0):
+    p = oracle_mod.phi4_params(shape, dtau, m2, lam, seed, C=C)
+    for s in range(steps):
+        phi = oracle_mod.phi4_step(p, phi, step0 + s)
+    return phi
+
+
+def _init(oracle_mod, shape, amp=0.9, seed=77):
+    p = oracle_mod.phi4_params(shape, 0.02, 0.5, 1.0, seed)
+    return oracle_mod.phi4_init(p, amp)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_noiseless_step_bitwise(gpu, oracle_mod, shape):
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, C=0.0) as L:
+        L.upload(phi0)
+        L.step(3)
+        got = L.download()
+    ref = _oracle_run(oracle_mod, shape, phi0, 3, C=0.0)
+    assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+def test_noisy_step_within_tolerance(gpu, oracle_mod, shape):
+    phi0 = _init(oracle_mod, shape)
+    k = 4
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(k)
+        got = L.download()
+    ref = _oracle_run(oracle_mod, shape, phi0, k)
+    err = np.abs(got.astype(np.float64) - ref)
+    bound = k * (STEP_ATOL + STEP_RTOL * np.abs(ref))
+    print(shape, "max err", err.max())
+    assert np.all(err <= bound)
+
+
+@pytest.mark.parametrize("shape,nslabs", [((16, 16, 16), 2), ((32, 8, 13), 3), ((256, 4, 33), 5),
+                                          ((64, 16, 8), 8), ((512, 4, 6), 2)])
+def test_loopback_decomposition_bitwise(gpu, oracle_mod, shape, nslabs):
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(7)
+        mono = L.download()
+    with _lat(shape, comm="loopback", nslabs=nslabs) as L:
+        L.upload(phi0)
+        L.step(7)
+        slabs = L.download()
+    assert np.array_equal(mono, slabs)
+
+
+def test_rccl_self_exchange_bitwise(gpu, oracle_mod):
+    from stochquant_amd import unique_id
+    shape = (64, 16, 12)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(5)
+        mono = L.download()
+    with _lat(shape, comm="rccl", nranks=1, rank=0, comm_id=unique_id()) as L:
+        L.upload(phi0)
+        L.step(5)
+        got = L.download()
+    assert np.array_equal(mono, got)
+
+
+def test_full_size_256_one_step(gpu, oracle_mod):
+    """BASELINE config C2 (256^3 fp32): one step vs the oracle, and the
+    decomposition invariance at full size."""
+    shape = (256, 256, 256)
+    phi0 = _init(oracle_mod, shape, amp=0.5)
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0) as L:
+        L.upload(phi0)
+        L.step(1)
+        got = L.download()
+    ref = _oracle_run(oracle_mod, shape, phi0, 1, dtau=0.01, m2=1.0, lam=1.0)
+    err = np.abs(got.astype(np.float64) - ref)
+    assert np.all(err <= STEP_ATOL + STEP_RTOL * np.abs(ref))
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, comm="loopback", nslabs=4) as L:
+        L.upload(phi0)
+        L.step(1)
+        assert np.array_equal(L.download(), got)
+
+
+def test_guard_clamp_nan_and_rollback(gpu, oracle_mod):
+    shape = (32, 8, 8)
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    phi0[3, 4, 5] = np.float32(5e3)
+    phi0[6, 1, 30] = np.float32("nan")
+    with _lat(shape, C=0.0, loops=3) as L:
+        L.upload(phi0)
+        L.step(1)
+        got = L.download()
+    ref = _oracle_run(oracle_mod, shape, phi0, 1, C=0.0)
+    assert np.array_equal(got, ref)
+    assert np.all(np.abs(got) <= 1000)
+    with _lat(shape, loops=3) as L:
+        L.upload(phi0)
+        d0 = L.dtau
+        stable = L.run_frame()
+        assert not stable
+        back = L.download()
+        assert np.array_equal(back[~np.isnan(phi0)], phi0[~np.isnan(phi0)])
+        assert np.isnan(back[6, 1, 30])
+        assert L.dtau == pytest.approx(d0 * 0.95)
+        assert L.step_counter == 3      # retried frames draw fresh noise
+
+
+def test_stable_frames_grow_dtau(gpu, oracle_mod):
+    shape = (16, 16, 16)
+    with _lat(shape, loops=5, dtau=0.01) as L:
+        L.init_field(0.2)
+        d0 = L.dtau
+        for _ in range(12):
+            assert L.run_frame()
+        assert L.dtau == pytest.approx(d0 / 0.95)  # tauhost.c:523-528: after 11 stable frames
+
+
+def test_init_field_matches_oracle(gpu, oracle_mod):
+    shape = (64, 16, 8)
+    with _lat(shape, seed=77) as L:
+        L.init_field(0.9)
+        got = L.download()
+    ref = _init(oracle_mod, shape, amp=0.9, seed=77)
+    assert np.all(np.abs(got - ref) <= 0.9 * (2e-6 + 2e-6 * np.abs(ref / 0.9)))
+
+
+def test_moments_and_correlator(gpu, oracle_mod):
+    shape = (32, 16, 24)
+    with _lat(shape) as L:
+        L.init_field(0.7)
+        L.step(3)
+        phi = L.download().astype(np.float64)
+        m = L.moments()
+        c = L.correlator(6)
+    assert m["sum"] == pytest.approx(phi.sum(), rel=1e-9, abs=1e-9)
+    assert m["sum2"] == pytest.approx((phi ** 2).sum(), rel=1e-9)
+    assert m["maxabs"] == np.abs(phi).max()
+    S = phi.sum(axis=(1, 2))
+    ref = np.array([np.sum(S * np.roll(S, -t)) for t in range(6)]) / phi.size
+    assert np.allclose(c, ref, rtol=1e-9)
+
+
+def test_free_field_variance_kat(gpu):
+    """lambda = 0: <phi^2> relaxes to the exact Euler-Maruyama value
+    mean_k [lam_k (1 - h lam_k/2)]^-1 (tests/golden/analytic_kats.json)."""
+    g = golden("analytic_kats.json")["free_var_3d_L32"]
+    L0 = g["L"]
+    with _lat((L0, L0, L0), dtau=g["h"], m2=g["m2"], lam=0.0, seed=4321) as L:
+        L.init_field(0.0)
+        L.step(500)
+        samples = []
+        for _ in range(200):
+            L.step(10)
+            samples.append(L.moments()["sum2"] / L0 ** 3)
+    s = np.array(samples)
+    blocks = s.reshape(20, 10).mean(axis=1)     # blocks of 100 steps ~ 1 autocorrelation time
+    err = blocks.std(ddof=1) / np.sqrt(len(blocks))
+    print("free var", s.mean(), "+-", err, "exact", g["value"])
+    assert abs(s.mean() - g["value"]) < 4 * err + 5e-4
+
+
+def test_unsupported_shape_fails_loudly(gpu):
+    from stochquant_amd import StochQuantError
+    with pytest.raises(StochQuantError):
+        _lat((20, 8, 8))

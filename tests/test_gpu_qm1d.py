@@ -1,0 +1,129 @@
+"""The reference model (QM1D, fp64) on the MI355X vs the oracle's Jacobi
+restatement (oracle/orc_qm1d.c, orc_qm1d_frame).
+
+Parity contract:
+  * potID 0, C = 0: bit-identical frame (f, x, xx0, omega, lrgEl, lrgVl,
+    stable) -- same fp64 operations in the reference's order.
+  * C = 1: the noise is the fp32 Box-Muller normal cast to double, exactly as
+    the reference's random() (tau_kernel.cl:277); GPU normals differ from the
+    oracle's by <= NORMAL bound, so |df| <= loops * sigma * 1.4e-5.
+  * potID 3: x_cl uses tanhf (tau_kernel.cl:187) whose device and glibc
+    versions differ by ~1 ulp fp32, so |df| <= loops * 2e-6.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_frame(N, a, h, pot, C, loops, seed, f, x, xx0, omega, runs=0, lrgEl=0, lrgVl=0.0, tick=0):
+    from stochquant_amd import Qm1dChain
+    with Qm1dChain(N, a, h, pot=pot, C=C, loops=loops, seed=seed, adapt_dtau=False) as q:
+        q.upload(f, x, xx0, omega, runs)
+        q.set_scan(lrgEl, lrgVl, tick)
+        stable = q.run_frame()
+        d = q.download()
+        sc = q.scan
+    return stable, d, sc
+
+
+def _state(N, seed=3, amp=0.05):
+    rng = np.random.default_rng(seed)
+    return rng.normal(0, amp, N), rng.normal(0, amp, N), rng.normal(0, amp, N)
+
+
+@pytest.mark.parametrize("N", [2, 3, 17, 100, 200, 1000, 1025, 4097, 8192])
+def test_ho_noiseless_frame_bitwise(gpu, oracle_mod, N):
+    a, h, loops = 0.1, 0.002, 50
+    f, x, xx0 = _state(N)
+    om = N * a / 2
+    stable, d, sc = _gpu_frame(N, a, h, 0, 0.0, loops, 9, f, x, xx0, om, runs=7, lrgVl=0.3)
+    r = oracle_mod.qm1d_frame(N, a, h, 0, 0.0, loops, 9, 0, 7, f, x, xx0, om, 0, 0.3)
+    assert stable == (r["stable"] == 1)
+    if stable:
+        assert np.array_equal(d["f"], r["f"])
+        assert np.array_equal(d["x"], r["x"])
+        assert np.array_equal(d["xx0"], r["xx0"])
+        assert d["omega"] == r["omega"]
+    assert sc["lrgEl"] == r["lrgEl"]
+    assert sc["lrgVl"] == r["lrgVl"]
+
+
+@pytest.mark.parametrize("N,pot,C", [(200, 0, 1.0), (1000, 0, 1.0), (200, 3, 0.0), (200, 3, 1.0),
+                                     (4096, 3, 1.0)])
+def test_frame_within_tolerance(gpu, oracle_mod, N, pot, C):
+    a, h, loops = 0.1, 0.002, 40
+    f, x, xx0 = _state(N)
+    om = N * a / 2 + 0.013
+    # lrgVl carried from earlier frames (a fresh 0 makes the first step's scan
+    # order-sensitive); 1.0 keeps these frames stable on both sides
+    stable, d, sc = _gpu_frame(N, a, h, pot, C, loops, 21, f, x, xx0, om, runs=3, lrgVl=1.0)
+    r = oracle_mod.qm1d_frame(N, a, h, pot, C, loops, 21, 0, 3, f, x, xx0, om, 0, 1.0)
+    assert r["stable"] == 1 and stable
+    sig = C * np.sqrt(np.float32(2 * h / a))
+    tol = loops * (sig * 1.4e-5 + 2e-6)
+    for k in ("f", "x", "xx0"):
+        err = np.max(np.abs(d[k] - r[k]))
+        print(k, err, tol)
+        assert err <= tol
+    assert abs(d["omega"] - r["omega"]) <= loops * 1e-5
+
+
+def test_unstable_frame_detected_and_rolled_back(gpu, oracle_mod):
+    """The double-well preset with Δτ/Δt² = 5 (taumain.py:101-108 at dt=0.02)
+    blows up in any ordering: both sides flag the frame, the state is kept."""
+    N, a, h, loops = 200, 0.02, 0.002, 10
+    f, x, xx0 = _state(N, amp=0.06)
+    om = 2.0
+    stable, d, sc = _gpu_frame(N, a, h, 3, 1.0, loops, 5, f, x, xx0, om)
+    r = oracle_mod.qm1d_frame(N, a, h, 3, 1.0, loops, 5, 0, 0, f, x, xx0, om)
+    assert r["stable"] == 0 and not stable
+    assert np.array_equal(d["f"], f)       # rollback: frame-start state kept
+    assert d["omega"] == om
+
+
+def test_ho_fixed_point_kat(gpu):
+    """C=0 gradient flow -> closed-form fixed point (oracle 1.04e-8)."""
+    from stochquant_amd import Qm1dChain
+    g = golden("analytic_kats.json")["ho_fixed_point"]
+    N = g["N"]
+    with Qm1dChain(N, g["a"], 0.002, pot=0, C=0.0, loops=1000, adapt_dtau=False) as q:
+        q.upload(np.zeros(N), omega=N * g["a"] / 2)
+        for _ in range(20):
+            assert q.run_frame()
+        f = q.download()["f"]
+    assert np.max(np.abs(f - np.array(g["f"]))) < 1e-8
+
+
+def test_free_chain_variance_kat(gpu):
+    """Bulk <f^2> of the HO chain (V''=2, a=1, h=0.01) -> 0.29378 (closed form)."""
+    from stochquant_amd import Qm1dChain
+    g = golden("analytic_kats.json")["free_var_1d"]
+    N = 8192
+    with Qm1dChain(N, 1.0, g["h"], pot=0, C=1.0, loops=50, seed=17, adapt_dtau=False) as q:
+        q.upload(np.zeros(N), omega=N / 2)
+        for _ in range(10):
+            q.run_frame()
+        vals = []
+        for _ in range(40):
+            assert q.run_frame()
+            f = q.download()["f"][64:-64]
+            vals.append(np.mean(f * f))
+    v = np.array(vals)
+    err = v.std(ddof=1) / np.sqrt(len(v))
+    print("chain var", v.mean(), "+-", err, "exact", g["value"])
+    assert abs(v.mean() - g["value"]) < 4 * err + 2e-3
+
+
+def test_dtau_controller(gpu):
+    from stochquant_amd import Qm1dChain
+    with Qm1dChain(100, 0.1, 0.002, pot=0, C=1.0, loops=5) as q:
+        q.upload(np.zeros(100), omega=5.0)
+        for _ in range(12):
+            assert q.run_frame()
+        assert q.dtau == pytest.approx(0.002 / 0.95)
+        q.dtau = 0.5        # Δτ/Δt² = 50: diverges
+        assert not q.run_frame()
+        assert q.dtau == pytest.approx(0.5 * 0.95)

@@ -1,0 +1,123 @@
+"""The oracle (CPU restatement, test infrastructure) pinned against every
+reference output that exists (tests/golden/reference_outputs.json) and the
+published Philox known-answer vectors, plus closed-form known answers."""
+import os
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+
+def run_ref(oracle_mod, tmp_path, argv):
+    """Run orc_tauhost with END/START placeholders mapped to files in tmp_path."""
+    a = ["end" if v == "END" else ("start" if v == "START" else v) for v in argv]
+    r = oracle_mod.tauhost(a, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr
+    end = (tmp_path / "end").read_text() if (tmp_path / "end").exists() else None
+    return r.stdout.decode(), end
+
+
+def test_philox_kat(oracle_mod):
+    for v in golden("philox_kat.json")["vectors"]:
+        ctr = [int(x, 16) for x in v["ctr"]]
+        key = [int(x, 16) for x in v["key"]]
+        out = oracle_mod.philox(ctr, key)
+        assert [f"{o:08x}" for o in out] == v["out"]
+
+
+def test_appendix_c_end_file_bit_exact(oracle_mod, tmp_path):
+    g = golden("reference_outputs.json")["appendix_c_end_file"]
+    out, end = run_ref(oracle_mod, tmp_path, g["argv"])
+    lines = end.split("\n")
+    assert lines[0] == g["first_line"]
+    assert lines[4:7] == g["trailer"]
+    stdout = out.split("\n")
+    assert stdout[0] == g["stdout_first_line"]
+    assert stdout[1].startswith(g["stdout_second_line_prefix"])
+
+
+def test_double_well_unstable_dtau_sequence(oracle_mod, tmp_path):
+    g = golden("reference_outputs.json")["double_well_all_unstable"]
+    out, end = run_ref(oracle_mod, tmp_path, g["argv"])
+    dt = [ln.split("|")[-2].strip() for ln in out.strip().split("\n")]
+    assert dt == g["printed_dtau"]
+    tail = end.strip().split("\n")[-3:]
+    assert float(tail[2].split("|")[0]) == pytest.approx(g["end_dtau"], rel=1e-6)
+    assert int(tail[1].split("|")[0]) == g["end_N"]
+
+
+def test_double_well_stable_and_resume_double_count(oracle_mod, tmp_path):
+    g = golden("reference_outputs.json")
+    _, end = run_ref(oracle_mod, tmp_path, g["double_well_stable"]["argv"])
+    assert int(end.strip().split("\n")[-2].split("|")[0]) == g["double_well_stable"]["end_N"]
+    shutil.copy(tmp_path / "end", tmp_path / "start")
+    _, end2 = run_ref(oracle_mod, tmp_path, g["resume_double_count"]["resume_argv"])
+    assert int(end2.strip().split("\n")[-2].split("|")[0]) == g["resume_double_count"]["resume_end_N"]
+
+
+def test_missing_start_file_error(oracle_mod, tmp_path):
+    r = oracle_mod.tauhost(["4", "0.5", "0.01", "1", "0", "1", "0", "1", "0", "5", "nope", "0", "12"],
+                           cwd=str(tmp_path))
+    assert r.returncode == 1
+    assert b"Failed to read Input." in r.stderr
+
+
+def test_ho_fixed_point_jacobi(oracle_mod):
+    """C=0 gradient flow converges to the closed-form fixed point."""
+    g = golden("analytic_kats.json")["ho_fixed_point"]
+    N = g["N"]
+    f = np.zeros(N)
+    x = np.zeros(N)
+    xx0 = np.zeros(N)
+    r = None
+    for frame in range(20):
+        r = oracle_mod.qm1d_frame(N, g["a"], 0.002, 0, 0.0, 1000, 1, frame * 1000, frame * 1000, f, x, xx0,
+                                  N * g["a"] / 2)
+        assert r["stable"] == 1
+        f, x, xx0 = r["f"], r["x"], r["xx0"]
+    assert np.max(np.abs(f - np.array(g["f"]))) < 1e-8
+
+
+def test_normals_statistics(oracle_mod):
+    z = oracle_mod.normals(1234, 0, 0, 7, 20000).astype(np.float64)
+    assert abs(z.mean()) < 0.02
+    assert abs(z.var() - 1) < 0.03
+    assert abs(np.mean(z ** 4) - 3) < 0.15
+    z2 = oracle_mod.normals(1234, 0, 0, 8, 20000)
+    assert abs(np.corrcoef(z, z2)[0, 1]) < 0.03
+
+
+def test_phi4_free_field_variance_oracle(oracle_mod):
+    """L=16 free field (lambda=0) relaxes to the exact Euler-Maruyama variance."""
+    g = golden("analytic_kats.json")["free_var_3d_L16"]
+    L = g["L"]
+    p = oracle_mod.phi4_params((L, L, L), g["h"], g["m2"], 0.0, 99)
+    phi = np.zeros((L, L, L), np.float32)
+    acc = []
+    for s in range(1200):
+        phi = oracle_mod.phi4_step(p, phi, s)
+        if s >= 400:
+            acc.append(float(np.mean(phi.astype(np.float64) ** 2)))
+    acc = np.array(acc)
+    # autocorrelation ~ 1/(h m2) = 100 steps -> ~8 independent blocks of 100
+    blocks = acc.reshape(8, 100).mean(axis=1)
+    err = blocks.std(ddof=1) / np.sqrt(len(blocks))
+    assert abs(acc.mean() - g["value"]) < 4 * err + 2e-3
+
+
+def test_phi4_slab_decomposition_matches_monolithic(oracle_mod):
+    """The ghost-plane slab form with global Philox indexing equals the periodic step bitwise."""
+    shape = (16, 8, 12)
+    p = oracle_mod.phi4_params(shape, 0.02, 0.5, 1.0, 7)
+    phi = oracle_mod.phi4_init(p, 0.7)
+    ref = oracle_mod.phi4_step(p, phi, 3)
+    Lz = shape[2]
+    for P in (1, 2, 3, 4):
+        parts = []
+        for r in range(P):
+            z0, z1 = Lz * r // P, Lz * (r + 1) // P
+            idx = [(z - 1) % Lz for z in range(z0, z1 + 2)]
+            parts.append(oracle_mod.phi4_step_slab(p, phi[idx], z0, 3))
+        assert np.array_equal(np.concatenate(parts), ref)
