@@ -128,8 +128,11 @@ int sq_set_step(sq_ctx *ctx, unsigned long long step);
  * S(z) = sum_{x,y} phi (single-slab contexts). */
 int sq_correlator(sq_ctx *ctx, double *out, int n);
 
-/* Profiling: per-launch hipEvents around every step kernel on its stream. */
-int sq_set_profiling(sq_ctx *ctx, int on);
+/* Profiling of the step kernels on their stream: mode 1 = every launch timed
+ * by hipExtLaunchKernel start/stop events (dispatch timestamps, no extra
+ * packets); mode 2 = one event pair around each sq_step call (region average,
+ * includes inter-kernel gaps); 0 = off.  Read with sq_perf. */
+int sq_set_profiling(sq_ctx *ctx, int mode);
 int sq_perf(sq_ctx *ctx, sq_perf_t *out);
 int sq_perf_reset(sq_ctx *ctx);
 int sq_sync(sq_ctx *ctx);

@@ -40,13 +40,13 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 }
 
 /* Box-Muller pair from two 32-bit words:
- *   u = (2*(w0>>9)+1) * 2^-24   in (0,1), exact in fp32
- *   t = (w1>>8) * 2^-24         in [0,1) revolutions, exact in fp32
+ *   u = 1 - (w0 & 0x7FFFFF) * 2^-23   in (0,1], exact in fp32
+ *   t = (w1 & 0x7FFFFF) * 2^-23       in [0,1) revolutions, exact in fp32
  *   n_cos = sqrt(-2 ln u) cos(2 pi t),  n_sin = sqrt(-2 ln u) sin(2 pi t) */
 static void bm_pair(uint32_t w0, uint32_t w1, float *nc, float *ns)
 {
-    const double u = (double)(2u * (w0 >> 9) + 1u) * 0x1p-24;
-    const double t = (double)(w1 >> 8) * 0x1p-24;
+    const double u = 1.0 - (double)(w0 & 0x7FFFFFu) * 0x1p-23;
+    const double t = (double)(w1 & 0x7FFFFFu) * 0x1p-23;
     const double r = sqrt(-2.0 * log(u));
     const double ang = 2.0 * M_PI * t;
     *nc = (float)(r * cos(ang));

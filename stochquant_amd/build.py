@@ -31,7 +31,8 @@ ARCH = os.environ.get("SQ_OFFLOAD_ARCH", "gfx950")
 DEVICE_SOURCES = ["sq_phi4.hip", "sq_qm1d.hip", "sq_selftest.hip"]
 HOST_SOURCES = ["sq_api.cpp"]
 HEADERS = ["sq_internal.h", "sq_rng.h"]
-COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-Wall", "-Wno-unused-function"]
+COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall",
+          "-Wno-unused-function"]
 
 
 def _digest(paths, extra):

@@ -108,10 +108,12 @@ struct sq_ctx {
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;
     ncclComm_t comm = nullptr;
-    // profiling
-    bool profiling = false;
+    // profiling: 0 off, 1 per launch (hipExtLaunchKernel dispatch timestamps),
+    // 2 one event pair around every sq_step call on the step-kernel stream
+    int profiling = 0;
     std::vector<EvPair> evpool;
     size_t ev_used = 0;
+    long long region_steps = 0;
     sq_perf_t perf{};
 };
 
@@ -127,13 +129,16 @@ int flush_events(sq_ctx *c) {
         c->perf.step_kernel_ms += ms;
         c->perf.step_kernel_launches += 1;
     }
+    if (c->region_steps > 0) {  // region mode: one pair per sq_step call covering its steps
+        c->perf.step_kernel_launches += c->region_steps - (long long)c->ev_used;
+        c->region_steps = 0;
+    }
     c->ev_used = 0;
     return SQ_OK;
 }
 
-int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
+int ev_take(sq_ctx *c, EvPair **out) {
     *out = nullptr;
-    if (!c->profiling) return SQ_OK;
     if (c->ev_used == c->evpool.size()) {
         if (c->evpool.size() >= 8192) {
             int rc = flush_events(c);
@@ -145,9 +150,17 @@ int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
             c->evpool.push_back(e);
         }
     }
-    EvPair *e = &c->evpool[c->ev_used++];
-    SQ_HIP(hipEventRecord(e->a, s));
-    *out = e;
+    *out = &c->evpool[c->ev_used++];
+    return SQ_OK;
+}
+
+// Marker-event pair around one launch (QM1D frames; per-launch mode only).
+int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
+    *out = nullptr;
+    if (c->profiling != 1) return SQ_OK;
+    int rc = ev_take(c, out);
+    if (rc) return rc;
+    SQ_HIP(hipEventRecord((*out)->a, s));
     return SQ_OK;
 }
 
@@ -184,12 +197,11 @@ int phi4_launch_range(sq_ctx *c, const Slab &s, hipStream_t st, int zlo, int zhi
     a.periodic = periodic;
     sq::phi4_fill_units(a, c->geom);
     EvPair *e = nullptr;
-    if (timed) {
-        int rc = ev_begin(c, st, &e);
+    if (timed && c->profiling == 1) {
+        int rc = ev_take(c, &e);
         if (rc) return rc;
     }
-    SQ_HIP(sq::phi4_step_launch(a, c->geom, st));
-    if (e) SQ_HIP(hipEventRecord(e->b, st));
+    SQ_HIP(sq::phi4_step_launch(a, c->geom, st, e ? e->a : nullptr, e ? e->b : nullptr));
     return SQ_OK;
 }
 
@@ -285,8 +297,16 @@ int create_phi4(sq_ctx *c) {
     if (!sq::phi4_geometry(c->Lx, c->Ly, &c->geom))
         return fail(SQ_E_ARG, "PHI4 needs Lx in {8,16,32,64,128,256} or a multiple of 256, and Ly a "
                               "multiple of the wave's row count");
-    if ((long long)c->Lx * c->Ly * c->Lz / 4 >= (1ll << 56))
-        return fail(SQ_E_ARG, "lattice too large for the Philox counter layout");
+    // Philox counter word 0 holds the global site quad (sites/4): < 2^32 quads,
+    // i.e. up to 1.7e10 sites (68 GB of fp32 field, a quarter of one MI355X).
+    if ((long long)c->Lx * c->Ly * c->Lz / 4 >= (1ll << 32))
+        return fail(SQ_E_ARG, "lattice exceeds 2^34 sites (Philox counter layout)");
+    if ((long long)c->Lx * c->Ly * 4 >= (1ll << 31))
+        return fail(SQ_E_ARG, "plane exceeds 2 GiB (32-bit buffer offsets)");
+    if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
+        const int r = atoi(e), rs = 64 / c->geom.qx;
+        if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0) c->geom = sq::Phi4Geom{c->geom.qx, r, rs * r};
+    }
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;
@@ -631,9 +651,19 @@ int sq_step(sq_ctx *c, int nsteps) {
     if (nsteps < 0) return fail(SQ_E_ARG, "nsteps < 0");
     DeviceGuard g(c->dev);
     const auto t0 = std::chrono::steady_clock::now();
+    EvPair *region = nullptr;
+    if (c->profiling == 2 && nsteps > 0) {
+        int rc = ev_take(c, &region);
+        if (rc) return rc;
+        SQ_HIP(hipEventRecord(region->a, c->slabs[0].sA));
+    }
     for (int i = 0; i < nsteps; ++i) {
         int rc = phi4_one_step(c);
         if (rc) return rc;
+    }
+    if (region) {
+        SQ_HIP(hipEventRecord(region->b, c->slabs[0].sA));
+        c->region_steps += nsteps;
     }
     c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return SQ_OK;
@@ -795,7 +825,10 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
 
 int sq_set_profiling(sq_ctx *c, int on) {
     if (!c) return fail(SQ_E_ARG, "null context");
-    c->profiling = on != 0;
+    if (on < 0 || on > 2) return fail(SQ_E_ARG, "profiling mode must be 0, 1 or 2");
+    int rc = flush_events(c);
+    if (rc) return rc;
+    c->profiling = on;
     return SQ_OK;
 }
 

@@ -34,7 +34,10 @@ struct Phi4Geom {
 bool phi4_geometry(int Lx, int Ly, Phi4Geom *g);
 // Fills the work decomposition of a launch that updates `nzc` chunks.
 void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g);
-hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s);
+// start/stop non-null: timed through hipExtLaunchKernel (timestamps of the
+// dispatch itself, no extra marker packets on the stream).
+hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s,
+                            hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
 // Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2, acc[2] = max |phi| (as

@@ -17,6 +17,8 @@
 // a block are independent, so a block's 4 waves take 4 y-adjacent units and
 // consecutive logical blocks are dealt to one XCD (T1 swizzle) so that the
 // halo rows and chunk-boundary planes they share hit that XCD's L2.
+#include <hip/hip_ext.h>
+
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -24,48 +26,173 @@ namespace sq {
 
 namespace {
 
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ float from_left_lane(float v) {  // lane i <- lane i-1 (mod 64)
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x13C, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x13C, 0xF, 0xF, true));
 }
 __device__ __forceinline__ float from_right_lane(float v) {  // lane i <- lane i+1 (mod 64)
-    return __builtin_bit_cast(
-        float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x134, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x134, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ float4 ld4(const float *p) { return *reinterpret_cast<const float4 *>(p); }
-__device__ __forceinline__ void st4(float *p, float4 v) { *reinterpret_cast<float4 *>(p) = v; }
+// Buffer descriptor over ONE plane: the base moves by scalar arithmetic per
+// plane and every per-lane offset (row within the plane) is loop-invariant,
+// so the z-march does no per-lane address math (guide T8/T20).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, int padded,
+                                                             size_t plane, uint32_t pbytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)padded * plane), (short)0,
+                                             (int)pbytes, 0x00020000);
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+    const f32x4v w = {v.x, v.y, v.z, v.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+}
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
 
-__device__ __forceinline__ const float *plane_ptr(const Phi4StepArgs &A, int zl, size_t plane) {
-    int p = zl + 1;  // padded index
+__device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
     if (A.periodic) {
-        if (zl < 0) p = A.nz;
-        else if (zl >= A.nz) p = 1;
+        if (zl < 0) return A.nz;
+        if (zl >= A.nz) return 1;
     }
-    return A.in + (size_t)p * plane;
+    return zl + 1;
 }
 
+// Guard of tau_kernel.cl:119-133 in two instructions: v_min_f32 returns the
+// non-NaN operand, so NaN -> +clamp, > clamp -> +clamp; then v_max_f32 gives
+// < -clamp -> -clamp.  Same results as the oracle's explicit branches.
 __device__ __forceinline__ float site_update(float phi, float xm, float xp, float ym, float yp,
-                                             float zm, float zp, float xi, const Phi4StepArgs &A,
-                                             int &bad) {
+                                             float zm, float zp, float xi, const Phi4StepArgs &A) {
     const float nb = ((xm + xp) + (ym + yp)) + (zm + zp);
     const float lap = __builtin_fmaf(-6.0f, phi, nb);
     const float g = __builtin_fmaf(A.lam6, phi * phi, A.m2);
     const float drift = __builtin_fmaf(-phi, g, lap);
     const float v = __builtin_fmaf(A.sig, xi, __builtin_fmaf(A.h, drift, phi));
-    const bool out = !(__builtin_fabsf(v) <= A.clampv);  // > clamp or NaN
-    bad |= (int)out;
-    const float gv = v < 0.0f ? -A.clampv : A.clampv;
-    return out ? gv : v;
+    return fmaxf(fminf(v, A.clampv), -A.clampv);
 }
 
+// Philox4x32-10 on R independent counters, round-major so the R dependency
+// chains interleave; the three-input xors are one v_bitop3_b32 each.
+template <int R>
+__device__ __forceinline__ void philox_rows(u32x4 (&c)[R], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int rnd = 0; rnd < 10; ++rnd) {
+        if (rnd) {
+            k0 += kPhiloxW0;
+            k1 += kPhiloxW1;
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t p0 = (uint64_t)kPhiloxM0 * c[r].x;
+            const uint64_t p1 = (uint64_t)kPhiloxM1 * c[r].z;
+            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c[r].y, k0, 0x96);
+            const uint32_t n2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c[r].w, k1, 0x96);
+            c[r] = u32x4{n0, (uint32_t)p1, n2, (uint32_t)p0};
+        }
+    }
+}
+
+template <int R>
+struct Slot {
+    float4 row[R];
+    float4 hm, hp;  // y-halo rows of the same plane
+};
+
 template <int QX, int R>
+struct Lane {
+    uint32_t voff[R];       // byte offset of the lane's float4 in each of its rows
+    uint32_t vm, vp;        // halo rows
+    uint32_t vl[R], vr[R];  // x-1 / x+4 neighbours across segment edges (multiseg)
+    uint32_t qoff[R];       // Philox quad offset inside the plane
+    bool rows_ok;
+    int lane;
+};
+
+template <int QX, int R>
+__device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, R> &L, Slot<R> &s,
+                                          int zl, bool halo, size_t plane, uint32_t pbytes) {
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, zl), plane, pbytes);
+#pragma unroll
+    for (int r = 0; r < R; ++r) s.row[r] = bload4(rs, L.voff[r]);
+    if (halo) {
+        s.hm = bload4(rs, L.vm);
+        s.hp = bload4(rs, L.vp);
+    }
+}
+
+// Update plane z from slots P (z-1), C (z), N (z+1); N is loaded here first.
+// MS: the row spans several 256-site wave segments (Lx > 256).
+template <int QX, int R, bool MS>
+__device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R> &L,
+                                           const Slot<R> &P, const Slot<R> &C, Slot<R> &N, int z,
+                                           int zend, size_t plane, uint32_t pbytes, uint32_t qplane,
+                                           int &bad) {
+    load_slot<QX, R>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+    float el[R], er[R];
+    if constexpr (MS) {
+        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, z), plane, pbytes);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            el[r] = 0.f;
+            er[r] = 0.f;
+            if (L.lane == 0) el[r] = bload1(rs, L.vl[r]);
+            if (L.lane == 63) er[r] = bload1(rs, L.vr[r]);
+        }
+    }
+    // noise for the R float4s of plane z: independent of the loads in flight
+    u32x4 c[R];
+    const uint32_t qbase = (uint32_t)(A.zg0 + z) * qplane;
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = u32x4{qbase + L.qoff[r], kStreamField << 24, A.s_lo, A.s_hi};
+    philox_rows<R>(c, A.k0, A.k1);
+    f32x4n xi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        box_muller(c[r].x, c[r].y, xi[r].a, xi[r].b);
+        box_muller(c[r].z, c[r].w, xi[r].c, xi[r].d);
+    }
+    const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, z + 1, plane, pbytes);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float4 cc = C.row[r];
+        const float4 up = r > 0 ? C.row[r > 0 ? r - 1 : 0] : C.hm;
+        const float4 dn = r < R - 1 ? C.row[r < R - 1 ? r + 1 : 0] : C.hp;
+        float lft, rgt;
+        if constexpr (QX == 64) {
+            lft = from_left_lane(cc.w);
+            rgt = from_right_lane(cc.x);
+        } else {
+            const int seg = L.lane & ~(QX - 1), xq = L.lane & (QX - 1);
+            lft = __shfl(cc.w, seg | ((xq + QX - 1) & (QX - 1)), 64);
+            rgt = __shfl(cc.x, seg | ((xq + 1) & (QX - 1)), 64);
+        }
+        if constexpr (MS) {
+            if (L.lane == 0) lft = el[r];
+            if (L.lane == 63) rgt = er[r];
+        }
+        float4 o;
+        o.x = site_update(cc.x, lft, cc.y, up.x, dn.x, P.row[r].x, N.row[r].x, xi[r].a, A);
+        o.y = site_update(cc.y, cc.x, cc.z, up.y, dn.y, P.row[r].y, N.row[r].y, xi[r].b, A);
+        o.z = site_update(cc.z, cc.y, cc.w, up.z, dn.z, P.row[r].z, N.row[r].z, xi[r].c, A);
+        o.w = site_update(cc.w, cc.z, rgt, up.w, dn.w, P.row[r].w, N.row[r].w, xi[r].d, A);
+        const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+        bad |= (int)(m >= A.clampv);
+        if (L.rows_ok) bstore4(ws, L.voff[r], o);
+    }
+}
+
+template <int QX, int R, bool MS>
 __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     constexpr int RS = 64 / QX;  // row sets per wave
-    const int lane = threadIdx.x & 63;
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
-    const int unit = lb * 4 + (int)(threadIdx.x >> 6);
+    // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
+    const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
     if (unit >= A.nunits) return;
     const int yg = unit % A.nyg;
     const int rest = unit / A.nyg;
@@ -76,103 +203,48 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
 
     const int Lx = A.Lx, Ly = A.Ly;
     const size_t plane = (size_t)Lx * (size_t)Ly;
-    const int xq = lane & (QX - 1);
-    const int rsid = lane / QX;
+    const uint32_t pbytes = (uint32_t)(plane * sizeof(float));
+    const uint32_t qplane = (uint32_t)(plane >> 2);
+    Lane<QX, R> L;
+    L.lane = threadIdx.x & 63;
+    const int xq = L.lane & (QX - 1);
+    const int rsid = L.lane / QX;
     const int x = xs * (4 * QX) + 4 * xq;
     // lanes whose rows fall past Ly (narrow lattices: a wave covers more rows
     // than Ly has) read row 0 and store nothing; shuffles stay inside their
     // x-segment group, which is idle as a whole.
     const int y0r = yg * (RS * R) + rsid * R;
-    const bool rows_ok = y0r < Ly;
-    const int y0 = rows_ok ? y0r : 0;
+    L.rows_ok = y0r < Ly;
+    const int y0 = L.rows_ok ? y0r : 0;
     const int ym = y0 == 0 ? Ly - 1 : y0 - 1;
     const int yp = (y0 + R == Ly) ? 0 : y0 + R;
-    const bool multiseg = A.nxseg > 1;  // only for QX == 64
     const int xl = (x == 0 ? Lx : x) - 1;
     const int xr = (x + 4 == Lx) ? 0 : x + 4;
-    const int seg_base = lane & ~(QX - 1);
-    const int src_l = seg_base | ((xq + QX - 1) & (QX - 1));
-    const int src_r = seg_base | ((xq + 1) & (QX - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        L.voff[r] = (uint32_t)(((y0 + r) * Lx + x) * 4);
+        L.vl[r] = (uint32_t)(((y0 + r) * Lx + xl) * 4);
+        L.vr[r] = (uint32_t)(((y0 + r) * Lx + xr) * 4);
+        L.qoff[r] = (uint32_t)(((y0 + r) * Lx + x) >> 2);
+    }
+    L.vm = (uint32_t)((ym * Lx + x) * 4);
+    L.vp = (uint32_t)((yp * Lx + x) * 4);
 
-    float4 pv[R], cv[R], nv[R];
-    float4 hm, hp, hm_n = make_float4(0, 0, 0, 0), hp_n = make_float4(0, 0, 0, 0);
-    {
-        const float *P = plane_ptr(A, zbeg - 1, plane);
-        const float *C = plane_ptr(A, zbeg, plane);
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            pv[r] = ld4(P + (size_t)(y0 + r) * Lx + x);
-            cv[r] = ld4(C + (size_t)(y0 + r) * Lx + x);
-        }
-        hm = ld4(C + (size_t)ym * Lx + x);
-        hp = ld4(C + (size_t)yp * Lx + x);
-    }
-    const uint64_t qplane = (uint64_t)(plane >> 2);
+    Slot<R> S0, S1, S2;
+    load_slot<QX, R>(A, L, S0, zbeg - 1, false, plane, pbytes);
+    load_slot<QX, R>(A, L, S1, zbeg, true, plane, pbytes);
     int bad = 0;
-    for (int z = zbeg; z < zend; ++z) {
-        const float *Np = plane_ptr(A, z + 1, plane);
-        const float *Cp = plane_ptr(A, z, plane);
-#pragma unroll
-        for (int r = 0; r < R; ++r) nv[r] = ld4(Np + (size_t)(y0 + r) * Lx + x);
-        const bool more = z + 1 < zend;
-        if (more) {
-            hm_n = ld4(Np + (size_t)ym * Lx + x);
-            hp_n = ld4(Np + (size_t)yp * Lx + x);
-        }
-        float el[R], er[R];
-        if (multiseg) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                el[r] = 0.f;
-                er[r] = 0.f;
-                if (lane == 0) el[r] = Cp[(size_t)(y0 + r) * Lx + xl];
-                if (lane == 63) er[r] = Cp[(size_t)(y0 + r) * Lx + xr];
-            }
-        }
-        // noise for the R float4s of plane z (independent of the loads above)
-        const uint64_t pq = (uint64_t)(A.zg0 + z) * qplane;
-        f32x4n xi[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const uint32_t off = (uint32_t)(((size_t)(y0 + r) * Lx + x) >> 2);
-            xi[r] = normals4(pq + off, kStreamField, A.s_lo, A.s_hi, A.k0, A.k1);
-        }
-        float *O = A.out + (size_t)(z + 1) * plane;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const float4 c = cv[r];
-            const float4 up = r > 0 ? cv[r > 0 ? r - 1 : 0] : hm;
-            const float4 dn = r < R - 1 ? cv[r < R - 1 ? r + 1 : 0] : hp;
-            float lft, rgt;
-            if constexpr (QX == 64) {
-                lft = from_left_lane(c.w);
-                rgt = from_right_lane(c.x);
-            } else {
-                lft = __shfl(c.w, src_l, 64);
-                rgt = __shfl(c.x, src_r, 64);
-            }
-            if (multiseg) {
-                if (lane == 0) lft = el[r];
-                if (lane == 63) rgt = er[r];
-            }
-            float4 o;
-            o.x = site_update(c.x, lft, c.y, up.x, dn.x, pv[r].x, nv[r].x, xi[r].a, A, bad);
-            o.y = site_update(c.y, c.x, c.z, up.y, dn.y, pv[r].y, nv[r].y, xi[r].b, A, bad);
-            o.z = site_update(c.z, c.y, c.w, up.z, dn.z, pv[r].z, nv[r].z, xi[r].c, A, bad);
-            o.w = site_update(c.w, c.z, rgt, up.w, dn.w, pv[r].w, nv[r].w, xi[r].d, A, bad);
-            if (rows_ok) st4(O + (size_t)(y0 + r) * Lx + x, o);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            pv[r] = cv[r];
-            cv[r] = nv[r];
-        }
-        hm = hm_n;
-        hp = hp_n;
+    // three-slot register queue, unrolled so no rotation moves are needed
+    for (int z = zbeg; z < zend; z += 3) {
+        plane_step<QX, R, MS>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+        if (z + 1 >= zend) break;
+        plane_step<QX, R, MS>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+        if (z + 2 >= zend) break;
+        plane_step<QX, R, MS>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
     }
-    if (!rows_ok) bad = 0;
+    if (!L.rows_ok) bad = 0;
     if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && lane == 0) atomicOr(A.flag, 1);
+        if (__ballot(bad) != 0ull && L.lane == 0) atomicOr(A.flag, 1);
     }
 }
 
@@ -185,7 +257,7 @@ __global__ __launch_bounds__(256) void phi4_init_kernel(float *slab, int Lx, int
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
          q += (size_t)gridDim.x * blockDim.x) {
         const f32x4n n = normals4(q0 + q, kStreamInit, 0u, 0u, k0, k1);
-        st4(slab + plane + 4 * q, make_float4(amp * n.a, amp * n.b, amp * n.c, amp * n.d));
+        *reinterpret_cast<float4 *>(slab + plane + 4 * q) = make_float4(amp * n.a, amp * n.b, amp * n.c, amp * n.d);
     }
 }
 
@@ -284,26 +356,39 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g) {
     a.nunits = a.nxseg * a.nyg * a.nzc;
 }
 
-template <int QX>
-static hipError_t launch_qx(const Phi4StepArgs &a, int r, dim3 grid, hipStream_t s) {
-    switch (r) {
-    case 4: hipLaunchKernelGGL((phi4_step_kernel<QX, 4>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((phi4_step_kernel<QX, 2>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((phi4_step_kernel<QX, 1>), grid, dim3(256), 0, s, a); break;
-    }
+template <int QX, int R, bool MS>
+static hipError_t launch_one(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
+                             hipEvent_t e1) {
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS>), grid, dim3(256), 0, s, e0, e1, 0, a);
+    else
+        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s) {
+template <int QX, bool MS>
+static hipError_t launch_qx(const Phi4StepArgs &a, int r, dim3 grid, hipStream_t s, hipEvent_t e0,
+                            hipEvent_t e1) {
+    switch (r) {
+    case 4: return launch_one<QX, 4, MS>(a, grid, s, e0, e1);
+    case 2: return launch_one<QX, 2, MS>(a, grid, s, e0, e1);
+    default: return launch_one<QX, 1, MS>(a, grid, s, e0, e1);
+    }
+}
+
+hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s, hipEvent_t e0,
+                            hipEvent_t e1) {
     if (a.nunits <= 0) return hipSuccess;
     const dim3 grid((unsigned)((a.nunits + 3) / 4));
     switch (g.qx) {
-    case 64: return launch_qx<64>(a, g.r, grid, s);
-    case 32: return launch_qx<32>(a, g.r, grid, s);
-    case 16: return launch_qx<16>(a, g.r, grid, s);
-    case 8: return launch_qx<8>(a, g.r, grid, s);
-    case 4: return launch_qx<4>(a, g.r, grid, s);
-    case 2: return launch_qx<2>(a, g.r, grid, s);
+    case 64:
+        return a.nxseg > 1 ? launch_qx<64, true>(a, g.r, grid, s, e0, e1)
+                           : launch_qx<64, false>(a, g.r, grid, s, e0, e1);
+    case 32: return launch_qx<32, false>(a, g.r, grid, s, e0, e1);
+    case 16: return launch_qx<16, false>(a, g.r, grid, s, e0, e1);
+    case 8: return launch_qx<8, false>(a, g.r, grid, s, e0, e1);
+    case 4: return launch_qx<4, false>(a, g.r, grid, s, e0, e1);
+    case 2: return launch_qx<2, false>(a, g.r, grid, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
 }

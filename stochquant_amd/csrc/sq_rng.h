@@ -9,7 +9,7 @@
 // order and any slab decomposition give the same numbers.
 //
 // Box-Muller on hardware transcendentals:
-//   u = (2*(w0>>9)+1)*2^-24  (exact fp32, in (0,1)),  t = (w1>>8)*2^-24 (exact)
+//   u = 1 - (w0 & 0x7FFFFF)*2^-23 in (0,1],  t = (w1 & 0x7FFFFF)*2^-23 (both exact)
 //   r = sqrt(-2 ln2 * log2 u)   v_log_f32 + v_sqrt_f32
 //   n = r*cos(2 pi t), r*sin(2 pi t)   v_cos_f32 / v_sin_f32 take revolutions,
 //   so no range reduction is needed.
@@ -56,8 +56,11 @@ __device__ __forceinline__ u32x4 philox_counter(uint64_t quad, uint32_t stream, 
 }
 
 __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float &nc, float &ns) {
-    const float u = (float)(((w0 >> 9) << 1) | 1u) * 0x1p-24f;
-    const float t = (float)(w1 >> 8) * 0x1p-24f;
+    // 23 mantissa bits of each word placed in [1,2) by one v_and_or_b32:
+    //   u = 2 - [1.m0] in (0,1] (exact, Sterbenz), t = [1.m1] in [1,2) revolutions;
+    //   cos/sin have period 1 revolution, so t needs no "- 1".
+    const float u = 2.0f - __uint_as_float(0x3F800000u | (w0 & 0x007FFFFFu));
+    const float t = __uint_as_float(0x3F800000u | (w1 & 0x007FFFFFu));
     const float r = __builtin_amdgcn_sqrtf(__builtin_amdgcn_logf(u) * -1.38629436111989061f);
     nc = r * __builtin_amdgcn_cosf(t);
     ns = r * __builtin_amdgcn_sinf(t);

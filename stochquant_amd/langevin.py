@@ -83,8 +83,9 @@ class _Ctx:
         _lib.call("sq_run_frame", self._h, ctypes.byref(st))
         return st.value == 1
 
-    def set_profiling(self, on=True):
-        _lib.call("sq_set_profiling", self._h, 1 if on else 0)
+    def set_profiling(self, mode=1):
+        """0 off; 1 every step kernel timed by dispatch events; 2 one event pair per step() call."""
+        _lib.call("sq_set_profiling", self._h, int(mode))
 
     def perf(self):
         p = _lib.SqPerf()

@@ -127,3 +127,32 @@ def test_dtau_controller(gpu):
         q.dtau = 0.5        # Δτ/Δt² = 50: diverges
         assert not q.run_frame()
         assert q.dtau == pytest.approx(0.5 * 0.95)
+
+
+def test_sampled_covariance_matches_exact_jacobi_law(gpu):
+    """Equal-time covariance of the GPU chain vs the exact stationary covariance
+    of the Jacobi Euler-Maruyama chain (discrete Lyapunov solution,
+    tests/qm1d_exact.py): the full stochastic behaviour of the kernel (drift,
+    noise amplitude sqrt(2h/a), boundary treatment) at 4 sigma."""
+    from qm1d_exact import stationary_cov
+    from stochquant_amd import Qm1dChain
+    N, a, h = 100, 0.1, 0.002
+    exact = stationary_cov(N, a, h, "jacobi")
+    with Qm1dChain(N, a, h, pot=0, C=1.0, loops=250, seed=99, adapt_dtau=False) as q:
+        q.upload(np.zeros(N), omega=5.0)
+        q.set_scan(0, 10.0, 0)
+        for _ in range(8):
+            q.run_frame()
+        F = []
+        for _ in range(600):
+            assert q.run_frame()
+            F.append(q.download()["f"])
+    F = np.array(F)
+    F -= F.mean(axis=0)
+    mid = N // 2
+    for j in (mid, mid - 5, mid + 10, 5):
+        prod = F[:, j] * F[:, mid]
+        b = prod.reshape(20, -1).mean(axis=1)
+        m, err = b.mean(), b.std(ddof=1) / np.sqrt(len(b))
+        print(j, m, "+-", err, "exact", exact[j, mid])
+        assert abs(m - exact[j, mid]) < 4 * err + 0.01

@@ -66,18 +66,20 @@ def test_stable_preset_and_resume(gpu, tmp_path):
     assert int(end2.strip().split("\n")[-2].split("|")[0]) == g["resume_double_count"]["resume_end_N"]
 
 
-def test_gpu_vs_reference_semantics_statistics(gpu, tmp_path, oracle_mod):
-    """Same CLI run through tauhost.o (GPU, Jacobi+Philox) and through the
-    serial reference restatement: the plotted correlator log|xavg| agrees in
-    the bulk within the statistical spread of two independent noise streams."""
-    argv = ["100", "0.1", "0.002", "30", "0", "1", "0", "1", "0", "1000", "0", "end", "17"]
-    out_gpu, _ = _run(tmp_path, argv)
-    r = oracle_mod.tauhost(argv, cwd=str(tmp_path))
-    assert r.returncode == 0
+def test_plotted_correlator_matches_exact_stationary_value(gpu, tmp_path):
+    """The curve taumain.py plots, log|xavg| (xavg = running <X_i X_mid> -
+    <X_i><X_mid>, tauhost.c:519-521), from a 60-frame tauhost.o run converges
+    to the exact stationary connected correlator of the Jacobi chain
+    (tests/qm1d_exact.py).  The reference's own ordering has a different
+    O(dtau) stationary law (Gauss-Seidel; checked against its exact value in
+    test_oracle.py), so the two runs are compared with their own exact laws,
+    not with each other.  ~150 independent samples -> 2.5 sigma = 30 %."""
+    from qm1d_exact import stationary_cov
     from stochquant_amd import parse_frame_line
-    yg = parse_frame_line(out_gpu.strip().split("\n")[-1].encode())["y"]
-    yr = parse_frame_line(r.stdout.decode().strip().split("\n")[-1].encode())["y"]
-    # xavg(i) ~ <X_i X_mid> - <X_i><X_mid>: compare the correlator near the midpoint
-    cg, cr = np.exp(yg[40:60]), np.exp(yr[40:60])
-    assert np.all(np.isfinite(cg)) and np.all(np.isfinite(cr))
-    assert abs(cg.mean() - cr.mean()) < 0.35 * max(cg.mean(), cr.mean())
+    argv = ["100", "0.1", "0.002", "60", "0", "1", "0", "1", "0", "1000", "0", "end", "17"]
+    out_gpu, _ = _run(tmp_path, argv)
+    y = parse_frame_line(out_gpu.strip().split("\n")[-1].encode())["y"]   # sites 1..N-1
+    c = np.exp(y[39:59])                                                    # sites 40..59
+    exact = stationary_cov(100, 0.1, 0.002, "jacobi")[40:60, 50]
+    assert np.all(np.isfinite(c))
+    assert abs(c.mean() - exact.mean()) < 0.3 * exact.mean()

@@ -121,3 +121,18 @@ def test_phi4_slab_decomposition_matches_monolithic(oracle_mod):
             idx = [(z - 1) % Lz for z in range(z0, z1 + 2)]
             parts.append(oracle_mod.phi4_step_slab(p, phi[idx], z0, 3))
         assert np.array_equal(np.concatenate(parts), ref)
+
+
+def test_serial_reference_order_matches_exact_gauss_seidel_law(oracle_mod, tmp_path):
+    """The reference semantics (serial restatement) relax to the exact
+    stationary law of the Gauss-Seidel-left Euler chain (tests/qm1d_exact.py):
+    the plotted connected correlator near the midpoint within 30 %."""
+    from qm1d_exact import stationary_cov
+    argv = ["100", "0.1", "0.002", "60", "0", "1", "0", "1", "0", "1000", "0", "0", "17"]
+    r = oracle_mod.tauhost(argv, cwd=str(tmp_path))
+    assert r.returncode == 0
+    last = r.stdout.decode().strip().split("\n")[-1]
+    y = np.genfromtxt([last.encode()], delimiter="|")[:-2]
+    c = np.exp(y[39:59])
+    exact = stationary_cov(100, 0.1, 0.002, "gs")[40:60, 50]
+    assert abs(c.mean() - exact.mean()) < 0.3 * exact.mean()
