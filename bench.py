@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU sample")
     ap.add_argument("--no-profile-events", action="store_true",
-                    help="time without per-launch events (roofline.achieved then uses wall time)")
+                    help="no hipEvents in the timed region (roofline.achieved then uses wall time)")
     return ap.parse_args()
 
 
@@ -117,7 +117,10 @@ def main():
     lat.sync()
     torch.cuda.synchronize()
     lat.perf_reset()
-    lat.set_profiling(not a.no_profile_events)
+    # mode 2: ONE hipEvent pair on the step-kernel stream around the K timed
+    # launches (per-launch dispatch events cost ~4 us of wall per step, see
+    # DESIGN.md §Measurement); avg launch = region / K, inter-kernel gaps included.
+    lat.set_profiling(0 if a.no_profile_events else 2)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -127,7 +130,7 @@ def main():
     barrier()
     t = time.perf_counter() - t0
     perf = lat.perf()
-    lat.set_profiling(False)
+    lat.set_profiling(0)
     if world > 1:
         tt = torch.tensor([t], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -183,7 +186,10 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(L, world),
-                "kernel": "phi4_step_kernel<64,4>",
+                "kernel": "phi4_step_kernel<QX=%d,R=%d,MS=%s> zc=%d" % (
+                    lat.tile[0], lat.tile[1], str(L > 256 and lat.tile[0] == 64).lower(), lat.tile[2]),
+                "timing": "hipEvent pair on the kernel stream around the timed launches (region mean)"
+                          if perf["step_kernel_launches"] > 0 else "wall clock",
                 "algorithmic_bytes_per_launch": BYTES_PER_SITE * sites_per_launch,
                 "avg_launch_us": round(avg_ms * 1e3, 3),
                 "launches_timed": perf["step_kernel_launches"],

@@ -1,0 +1,78 @@
+"""Turn two rocprofv3 --pmc runs (FETCH_SIZE, WRITE_SIZE; separate passes,
+MI355X_MICROARCH.md §rocprofv3 PMC slots) into HBM bytes per launch of the
+phi^4 step kernel, and write profiles/pmc_traffic.json for bench.py.
+
+gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts the
+L2's memory-side read requests at 64 B but wide streaming reads issue 128-B
+requests, so it reports exactly half the bytes: multiply by 2.  WRITE_SIZE
+(KiB) is exact for 16-B-per-lane streaming stores.  Infinity-Cache hits are
+counted, so at 256^3 (working set < 256 MiB) this is L2-miss traffic, not
+strictly DRAM traffic.
+
+    python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR --size 256 [--out profiles/pmc_traffic.json]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def counter_values(d, counter, kernel_substr="phi4_step_kernel"):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    vals = []
+    kname = None
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if kernel_substr in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                    vals.append(float(row["Counter_Value"]))
+                    kname = row["Kernel_Name"]
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kernel_substr} in {files}")
+    return vals, kname
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "profiles", "pmc_traffic.json"))
+    a = ap.parse_args()
+    fv, kname = counter_values(a.fetch_dir, "FETCH_SIZE")
+    wv, _ = counter_values(a.write_dir, "WRITE_SIZE")
+    # drop the first launches (cold caches) when there are enough samples
+    fv_s = fv[len(fv) // 5:] if len(fv) >= 10 else fv
+    wv_s = wv[len(wv) // 5:] if len(wv) >= 10 else wv
+    fetch_kib = statistics.median(fv_s)
+    write_kib = statistics.median(wv_s)
+    read_bytes = 2.0 * fetch_kib * 1024
+    write_bytes = write_kib * 1024
+    alg = 8 * a.size ** 3
+    out = {
+        "size": a.size,
+        "nranks": a.nranks,
+        "kernel": kname,
+        "launches_fetch": len(fv), "launches_write": len(wv),
+        "FETCH_SIZE_KiB_median": fetch_kib,
+        "WRITE_SIZE_KiB_median": write_kib,
+        "read_bytes_per_launch": read_bytes,
+        "write_bytes_per_launch": write_bytes,
+        "hbm_bytes_per_launch": read_bytes + write_bytes,
+        "algorithmic_bytes_per_launch": alg,
+        "traffic_over_algorithmic": (read_bytes + write_bytes) / alg,
+        "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB x1024",
+    }
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -89,6 +89,7 @@ SIGNATURES = {
     "sq_init_field": (ctypes.c_int, [_P, ctypes.c_float]),
     "sq_slab": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     "sq_moments": (ctypes.c_int, [_P, _D]),
+    "sq_phi4_tile": (ctypes.c_int, [_P, _I]),
     "sq_set_dtau": (ctypes.c_int, [_P, ctypes.c_double]),
     "sq_get_dtau": (ctypes.c_int, [_P, _D]),
     "sq_get_step": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),

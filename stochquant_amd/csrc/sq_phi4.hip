@@ -334,7 +334,11 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     else if (Lx < 256 && Lx >= 8 && 64 % (Lx / 4) == 0) qx = Lx / 4;
     else return false;
     const int rs = 64 / qx;
-    static const int rcand[3] = {4, 2, 1};
+    // Rows per lane (measured, profiles/r01/sweep*): one row per lane wins when
+    // a wave spans the whole x row (more waves in flight, fewer VGPRs); with
+    // several x segments per row two rows amortise the segment-edge loads.
+    const bool one_seg = Lx <= 256;
+    const int rcand[3] = {one_seg ? 1 : 2, one_seg ? 2 : 4, one_seg ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
         if (Ly % (rs * r) == 0) {
             *g = Phi4Geom{qx, r, rs * r};

@@ -38,11 +38,28 @@ __global__ void philox_kernel(const uint32_t *ck, uint32_t *out) {
     out[3] = o.w;
 }
 
-__global__ __launch_bounds__(256) void copy_kernel(const float4 *__restrict__ in,
-                                                   float4 *__restrict__ out, size_t n4) {
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-         i += (size_t)gridDim.x * blockDim.x)
-        out[i] = in[i];
+// Streaming copy used as the measured HBM ceiling: every thread moves 4
+// float4 (all four loads issued before the stores), one pass, no grid-stride;
+// NT = non-temporal loads/stores.  sq_copy_bandwidth reports the faster.
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ __launch_bounds__(256) void copy_kernel(const f4v *__restrict__ in, f4v *__restrict__ out,
+                                                   size_t n4) {
+    const size_t base = (size_t)blockIdx.x * 1024 + threadIdx.x;
+    f4v v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const size_t i = base + 256 * k;
+        if (i < n4) v[k] = NT ? __builtin_nontemporal_load(in + i) : in[i];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const size_t i = base + 256 * k;
+        if (i < n4) {
+            if (NT) __builtin_nontemporal_store(v[k], out + i);
+            else out[i] = v[k];
+        }
+    }
 }
 
 }  // namespace
@@ -66,9 +83,12 @@ hipError_t selftest_philox_launch(const uint32_t *ck, uint32_t *out, hipStream_t
     return hipGetLastError();
 }
 
-hipError_t copy_launch(const float4 *in, float4 *out, size_t n4, hipStream_t s) {
-    const unsigned grid = (unsigned)std::min<size_t>((n4 + 255) / 256, 256 * 8);
-    hipLaunchKernelGGL(copy_kernel, dim3(grid), dim3(256), 0, s, in, out, n4);
+hipError_t copy_launch(const float4 *in, float4 *out, size_t n4, bool nt, hipStream_t s) {
+    const unsigned grid = (unsigned)((n4 + 1023) / 1024);
+    const f4v *i4 = reinterpret_cast<const f4v *>(in);
+    f4v *o4 = reinterpret_cast<f4v *>(out);
+    if (nt) hipLaunchKernelGGL(copy_kernel<true>, dim3(grid), dim3(256), 0, s, i4, o4, n4);
+    else hipLaunchKernelGGL(copy_kernel<false>, dim3(grid), dim3(256), 0, s, i4, o4, n4);
     return hipGetLastError();
 }
 

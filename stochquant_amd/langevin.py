@@ -214,6 +214,13 @@ class Phi4Lattice(_Ctx):
         _lib.call("sq_moments", self._h, _dptr(out))
         return {"sum": out[0], "sum2": out[1], "maxabs": out[2]}
 
+    @property
+    def tile(self):
+        """(lanes per x segment, rows per lane, z planes per wave) of the step kernel."""
+        out = (ctypes.c_int * 3)()
+        _lib.call("sq_phi4_tile", self._h, out)
+        return tuple(out)
+
     def correlator(self, n=None):
         n = self.shape[2] if n is None else int(n)
         out = np.empty(n)
