@@ -362,6 +362,7 @@ int create_phi4(sq_ctx *c) {
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     c->zc = zc;
+    SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
 }
 
@@ -385,6 +386,7 @@ int create_qm1d(sq_ctx *c) {
     }
     SQ_HIP(hipMalloc(&c->qst, sizeof(sq::Qm1dState)));
     SQ_HIP(hipStreamCreateWithFlags(&c->qstream, hipStreamNonBlocking));
+    SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
 }
 
@@ -752,8 +754,8 @@ int sq_moments(sq_ctx *c, double out[3]) {
     const size_t plane = plane_floats(c);
     out[0] = out[1] = out[2] = 0;
     for (auto &s : c->slabs) {
-        SQ_HIP(hipMemset(c->dacc, 0, 2 * sizeof(double)));
-        SQ_HIP(hipMemset(c->dmax, 0, sizeof(unsigned int)));
+        SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));  // same stream as the kernel:
+        SQ_HIP(hipMemsetAsync(c->dmax, 0, sizeof(unsigned int), s.sA));  // the null stream does not order non-blocking streams
         SQ_HIP(sq::phi4_moments_launch(s.buf[c->cur] + plane, (long long)s.nz * (long long)plane,
                                        c->dacc, c->dmax, s.sA));
         double acc[2];
