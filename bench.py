@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--size", type=int, default=256, help="per-GPU lattice edge (default 256 = config C2)")
     ap.add_argument("--dtau", type=float, default=0.01)
+    ap.add_argument("--comm", choices=["auto", "rccl", "loopback"], default="auto",
+                    help="auto: one slab at N=1, RCCL slabs at N>1; rccl/loopback force the slab path "
+                         "at N=1 (RCCL self-exchange / --slabs slabs on one GPU) to exercise it")
+    ap.add_argument("--slabs", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU sample")
     ap.add_argument("--no-profile-events", action="store_true",
@@ -105,8 +109,13 @@ def main():
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         lat = Phi4Lattice(shape, comm="rccl", nranks=world, rank=rank, comm_id=obj[0], **kw)
+    elif a.comm == "rccl":
+        lat = Phi4Lattice(shape, comm="rccl", nranks=1, rank=0, comm_id=unique_id(), **kw)
+    elif a.comm == "loopback":
+        lat = Phi4Lattice(shape, comm="loopback", nslabs=a.slabs, **kw)
     else:
         lat = Phi4Lattice(shape, **kw)
+    slab_path = world > 1 or a.comm != "auto"
     lat.init_field(0.1)
 
     def barrier():
@@ -141,8 +150,10 @@ def main():
     total_updates = float(L ** 3) * world * a.steps
     value = total_updates / t
     if perf["step_kernel_launches"] > 0:
+        # region mean per step on the (interior) step-kernel stream; with slabs it
+        # spans interior + halo + boundary, so charge all local sites to it
         avg_ms = perf["step_kernel_ms"] / perf["step_kernel_launches"]
-        sites_per_launch = sites_local if world == 1 else (lat.nz_local - 2) * L * L
+        sites_per_launch = sites_local
     else:
         avg_ms = t * 1e3 / a.steps
         sites_per_launch = sites_local
@@ -176,8 +187,9 @@ def main():
                 "lattice": list(shape),
                 "per_gpu": [L, L, L],
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
-                "parallelism": "single GPU, one stream" if world == 1 else
-                               f"z-slab x{world}, RCCL halo on stream B, interior on stream A",
+                "parallelism": "single GPU, one stream" if not slab_path else
+                               f"z-slab x{world} ({a.comm if world == 1 else 'rccl'}), halo + boundary planes on "
+                               f"stream B, interior on stream A",
             },
             "roofline": {
                 "bound": "hbm",

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--rows", default="1,2,4")
     ap.add_argument("--zc", default="2,4,8,16")
+    ap.add_argument("--C", type=float, default=1.0, help="noise amplitude (0: RNG-free gradient-flow kernel)")
     a = ap.parse_args()
     from stochquant_amd import Phi4Lattice
     L = a.size
@@ -30,7 +31,7 @@ def main():
     lats = {}
     for v in variants:
         os.environ["SQ_ROWS"], os.environ["SQ_ZCHUNK"] = str(v[0]), str(v[1])
-        lat = Phi4Lattice((L, L, L), dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED)
+        lat = Phi4Lattice((L, L, L), dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, C=a.C)
         lat.init_field(0.1)
         lat.step(50)
         lat.sync()

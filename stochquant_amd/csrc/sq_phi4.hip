@@ -66,13 +66,15 @@ __device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
 // Guard of tau_kernel.cl:119-133 in two instructions: v_min_f32 returns the
 // non-NaN operand, so NaN -> +clamp, > clamp -> +clamp; then v_max_f32 gives
 // < -clamp -> -clamp.  Same results as the oracle's explicit branches.
+template <bool NZ>
 __device__ __forceinline__ float site_update(float phi, float xm, float xp, float ym, float yp,
                                              float zm, float zp, float xi, const Phi4StepArgs &A) {
     const float nb = ((xm + xp) + (ym + yp)) + (zm + zp);
     const float lap = __builtin_fmaf(-6.0f, phi, nb);
     const float g = __builtin_fmaf(A.lam6, phi * phi, A.m2);
     const float drift = __builtin_fmaf(-phi, g, lap);
-    const float v = __builtin_fmaf(A.sig, xi, __builtin_fmaf(A.h, drift, phi));
+    const float det = __builtin_fmaf(A.h, drift, phi);
+    const float v = NZ ? __builtin_fmaf(A.sig, xi, det) : det;  // NZ = false: C = 0 gradient flow
     return fmaxf(fminf(v, A.clampv), -A.clampv);
 }
 
@@ -127,7 +129,8 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 
 // Update plane z from slots P (z-1), C (z), N (z+1); N is loaded here first.
 // MS: the row spans several 256-site wave segments (Lx > 256).
-template <int QX, int R, bool MS>
+// NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
+template <int QX, int R, bool MS, bool NZ>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R> &L,
                                            const Slot<R> &P, const Slot<R> &C, Slot<R> &N, int z,
                                            int zend, size_t plane, uint32_t pbytes, uint32_t qplane,
@@ -145,16 +148,21 @@ __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX,
         }
     }
     // noise for the R float4s of plane z: independent of the loads in flight
-    u32x4 c[R];
-    const uint32_t qbase = (uint32_t)(A.zg0 + z) * qplane;
-#pragma unroll
-    for (int r = 0; r < R; ++r) c[r] = u32x4{qbase + L.qoff[r], kStreamField << 24, A.s_lo, A.s_hi};
-    philox_rows<R>(c, A.k0, A.k1);
     f32x4n xi[R];
+    if constexpr (NZ) {
+        u32x4 c[R];
+        const uint32_t qbase = (uint32_t)(A.zg0 + z) * qplane;
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-        box_muller(c[r].x, c[r].y, xi[r].a, xi[r].b);
-        box_muller(c[r].z, c[r].w, xi[r].c, xi[r].d);
+        for (int r = 0; r < R; ++r) c[r] = u32x4{qbase + L.qoff[r], kStreamField << 24, A.s_lo, A.s_hi};
+        philox_rows<R>(c, A.k0, A.k1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            box_muller(c[r].x, c[r].y, xi[r].a, xi[r].b);
+            box_muller(c[r].z, c[r].w, xi[r].c, xi[r].d);
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < R; ++r) xi[r] = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
     const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, z + 1, plane, pbytes);
 #pragma unroll
@@ -176,17 +184,17 @@ __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX,
             if (L.lane == 63) rgt = er[r];
         }
         float4 o;
-        o.x = site_update(cc.x, lft, cc.y, up.x, dn.x, P.row[r].x, N.row[r].x, xi[r].a, A);
-        o.y = site_update(cc.y, cc.x, cc.z, up.y, dn.y, P.row[r].y, N.row[r].y, xi[r].b, A);
-        o.z = site_update(cc.z, cc.y, cc.w, up.z, dn.z, P.row[r].z, N.row[r].z, xi[r].c, A);
-        o.w = site_update(cc.w, cc.z, rgt, up.w, dn.w, P.row[r].w, N.row[r].w, xi[r].d, A);
+        o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[r].x, N.row[r].x, xi[r].a, A);
+        o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[r].y, N.row[r].y, xi[r].b, A);
+        o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[r].z, N.row[r].z, xi[r].c, A);
+        o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[r].w, N.row[r].w, xi[r].d, A);
         const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
         bad |= (int)(m >= A.clampv);
         if (L.rows_ok) bstore4(ws, L.voff[r], o);
     }
 }
 
-template <int QX, int R, bool MS>
+template <int QX, int R, bool MS, bool NZ>
 __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     constexpr int RS = 64 / QX;  // row sets per wave
     const int nb = gridDim.x, b = blockIdx.x;
@@ -236,11 +244,11 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     int bad = 0;
     // three-slot register queue, unrolled so no rotation moves are needed
     for (int z = zbeg; z < zend; z += 3) {
-        plane_step<QX, R, MS>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+        plane_step<QX, R, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
         if (z + 1 >= zend) break;
-        plane_step<QX, R, MS>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+        plane_step<QX, R, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
         if (z + 2 >= zend) break;
-        plane_step<QX, R, MS>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+        plane_step<QX, R, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
     }
     if (!L.rows_ok) bad = 0;
     if (A.flag != nullptr) {
@@ -360,14 +368,21 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g) {
     a.nunits = a.nxseg * a.nyg * a.nzc;
 }
 
+template <int QX, int R, bool MS, bool NZ>
+static hipError_t launch_nz(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
+                            hipEvent_t e1) {
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ>), grid, dim3(256), 0, s, e0, e1, 0, a);
+    else
+        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 template <int QX, int R, bool MS>
 static hipError_t launch_one(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
                              hipEvent_t e1) {
-    if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS>), grid, dim3(256), 0, s, e0, e1, 0, a);
-    else
-        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
+    return a.sig != 0.0f ? launch_nz<QX, R, MS, true>(a, grid, s, e0, e1)
+                         : launch_nz<QX, R, MS, false>(a, grid, s, e0, e1);
 }
 
 template <int QX, bool MS>
