@@ -65,7 +65,7 @@ struct Slab {
     int nz = 0;
     long long z0 = 0;
     hipStream_t sA = nullptr, sB = nullptr;
-    hipEvent_t evA = nullptr, evB = nullptr, evPush = nullptr;
+    hipEvent_t evA = nullptr, evC = nullptr;  // A: block's steps done; C: its halo exchange done
 };
 
 struct EvPair {
@@ -102,6 +102,7 @@ struct sq_ctx {
     long long Lz = 0;
     sq::Phi4Geom geom{};
     int zc = 8;
+    int gz = 1;  // ghost-zone depth (planes) of slab decompositions = steps per halo exchange
     std::vector<Slab> slabs;
     int cur = 0;
     int *flag = nullptr;
@@ -164,14 +165,21 @@ int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
     return SQ_OK;
 }
 
-sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s) {
+size_t plane_floats(const sq_ctx *c) { return (size_t)c->Lx * (size_t)c->Ly; }
+
+// Local plane 0 of buffer k (the ghost zone is the c->gz planes on either side).
+float *plane0(const sq_ctx *c, const Slab &s, int k) { return s.buf[k] + (size_t)c->gz * plane_floats(c); }
+
+sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     sq::Phi4StepArgs a{};
-    a.in = s.buf[c->cur];
-    a.out = s.buf[c->cur ^ 1];
+    a.in = s.buf[in_buf];
+    a.out = s.buf[in_buf ^ 1];
     a.Lx = c->Lx;
     a.Ly = c->Ly;
     a.nz = s.nz;
+    a.gz = c->gz;
     a.zg0 = s.z0;
+    a.Lzg = c->Lz;
     const float h = (float)c->dtau;
     a.h = h;
     a.m2 = (float)c->p.m2;
@@ -186,9 +194,11 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s) {
     return a;
 }
 
-int phi4_launch_range(sq_ctx *c, const Slab &s, hipStream_t st, int zlo, int zhi, int zstep,
-                      int zc, int nzc, int periodic, bool timed) {
-    sq::Phi4StepArgs a = phi4_base_args(c, s);
+// Update local planes of the given chunks: chunk k = [zlo + k*zstep, +zc) clipped to zhi.
+int phi4_launch_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo, int zhi,
+                      int zstep, int zc, int nzc, int periodic, bool timed) {
+    if (nzc <= 0 || zhi <= zlo) return SQ_OK;
+    sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
     a.zlo = zlo;
     a.zhi = zhi;
     a.zstep = zstep;
@@ -205,76 +215,132 @@ int phi4_launch_range(sq_ctx *c, const Slab &s, hipStream_t st, int zlo, int zhi
     return SQ_OK;
 }
 
-size_t plane_floats(const sq_ctx *c) { return (size_t)c->Lx * (size_t)c->Ly; }
+// Planes [lo, hi) in chunks of c->zc.
+int phi4_launch_span(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo, int hi, bool timed) {
+    if (hi <= lo) return SQ_OK;
+    return phi4_launch_range(c, s, in_buf, st, lo, hi, c->zc, c->zc, (hi - lo + c->zc - 1) / c->zc, 0, timed);
+}
 
-// One Langevin step of every slab.
-int phi4_one_step(sq_ctx *c) {
-    const size_t plane = plane_floats(c);
-    const size_t pbytes = plane * sizeof(float);
-    if (c->p.comm == SQ_COMM_NONE) {
-        Slab &s = c->slabs[0];
-        const int nzc = (s.nz + c->zc - 1) / c->zc;
-        int rc = phi4_launch_range(c, s, s.sA, 0, s.nz, c->zc, c->zc, nzc, 1, true);
-        if (rc) return rc;
-    } else {
-        const int ns = (int)c->slabs.size();
-        // 1. halo exchange into the ghosts of the CURRENT buffers (stream B)
-        if (c->p.comm == SQ_COMM_LOOPBACK) {
-            for (int i = 0; i < ns; ++i) {
-                Slab &s = c->slabs[i];
-                Slab &dn = c->slabs[(i + ns - 1) % ns];
-                Slab &up = c->slabs[(i + 1) % ns];
-                float *cur = s.buf[c->cur];
-                // my plane 0 -> lower neighbour's upper ghost; my top plane -> upper's lower ghost
-                SQ_HIP(hipMemcpyAsync(dn.buf[c->cur] + (size_t)(dn.nz + 1) * plane, cur + plane,
-                                      pbytes, hipMemcpyDeviceToDevice, s.sB));
-                SQ_HIP(hipMemcpyAsync(up.buf[c->cur], cur + (size_t)s.nz * plane, pbytes,
-                                      hipMemcpyDeviceToDevice, s.sB));
-                SQ_HIP(hipEventRecord(s.evPush, s.sB));
-                c->perf.halo_bytes += 2.0 * (double)pbytes;
-            }
-            for (int i = 0; i < ns; ++i) {
-                Slab &s = c->slabs[i];
-                SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evPush, 0));
-                SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evPush, 0));
-            }
-        } else {  // RCCL: one slab per process
-            Slab &s = c->slabs[0];
-            float *cur = s.buf[c->cur];
-            const int P = c->p.nranks, r = c->p.rank;
-            const int up = (r + 1) % P, dn = (r + P - 1) % P;
-            SQ_NCCL(ncclGroupStart());
-            SQ_NCCL(ncclSend(cur + (size_t)s.nz * plane, plane, ncclFloat32, up, c->comm, s.sB));
-            SQ_NCCL(ncclSend(cur + plane, plane, ncclFloat32, dn, c->comm, s.sB));
-            SQ_NCCL(ncclRecv(cur, plane, ncclFloat32, dn, c->comm, s.sB));
-            SQ_NCCL(ncclRecv(cur + (size_t)(s.nz + 1) * plane, plane, ncclFloat32, up, c->comm, s.sB));
-            SQ_NCCL(ncclGroupEnd());
-            c->perf.halo_bytes += 2.0 * (double)pbytes;
-        }
-        // 2. boundary planes on B (after the interior kernel of the previous step read them)
-        for (auto &s : c->slabs) {
-            SQ_HIP(hipStreamWaitEvent(s.sB, s.evA, 0));
-            const int nzc = s.nz > 1 ? 2 : 1;
-            int rc = phi4_launch_range(c, s, s.sB, 0, s.nz, std::max(1, s.nz - 1), 1, nzc, 0, false);
-            if (rc) return rc;
-        }
-        // 3. interior planes on A (after the boundary kernel of the previous step)
-        for (auto &s : c->slabs) {
-            SQ_HIP(hipStreamWaitEvent(s.sA, s.evB, 0));
-            if (s.nz > 2) {
-                const int n = s.nz - 2;
-                const int nzc = (n + c->zc - 1) / c->zc;
-                int rc = phi4_launch_range(c, s, s.sA, 1, s.nz - 1, c->zc, c->zc, nzc, 0, true);
-                if (rc) return rc;
-            }
-            SQ_HIP(hipEventRecord(s.evA, s.sA));
-        }
-        for (auto &s : c->slabs) SQ_HIP(hipEventRecord(s.evB, s.sB));
-    }
-    c->cur ^= 1;
+void count_step(sq_ctx *c) {
     c->step += 1;
     c->perf.steps += 1;
-    for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane;
+    for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane_floats(c);
+}
+
+// Single slab covering the lattice: one launch per step, z wraps in-kernel.
+int phi4_periodic_step(sq_ctx *c) {
+    Slab &s = c->slabs[0];
+    const int nzc = (s.nz + c->zc - 1) / c->zc;
+    int rc = phi4_launch_range(c, s, c->cur, s.sA, 0, s.nz, c->zc, c->zc, nzc, 1, true);
+    if (rc) return rc;
+    c->cur ^= 1;
+    count_step(c);
+    return SQ_OK;
+}
+
+// Deep-halo block of g <= gz steps on every slab.
+//   stream B: after the previous block (evA), exchange gz edge planes of the
+//             current buffer with both z-neighbours (RCCL or D2D), record evC;
+//   stream A: step 0 on the planes that need no ghost, [1, nz-1), overlapped
+//             with the exchange; then (after evC) step 0 on the rim
+//             [-(g-1), 1) u [nz-1, nz+g-1); then steps s = 1..g-1 on the
+//             shrinking extended range [-(g-1-s), nz+g-1-s); record evA.
+// Ghost-zone sites are recomputed redundantly; the counter-based noise makes
+// them bit-identical to their owner's, so the result equals the monolithic run.
+int phi4_block(sq_ctx *c, int g) {
+    const size_t plane = plane_floats(c);
+    const int ns = (int)c->slabs.size(), G = c->gz;
+    const size_t gbytes = (size_t)G * plane * sizeof(float);
+    const int cur = c->cur;
+    // 1. exchange (stream B)
+    for (int i = 0; i < ns; ++i) {
+        Slab &s = c->slabs[i];
+        SQ_HIP(hipStreamWaitEvent(s.sB, s.evA, 0));
+        if (c->p.comm == SQ_COMM_LOOPBACK) {  // we write the neighbours' ghosts: wait for them too
+            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evA, 0));
+            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evA, 0));
+        }
+    }
+    if (c->p.comm == SQ_COMM_LOOPBACK) {
+        for (int i = 0; i < ns; ++i) {
+            Slab &s = c->slabs[i];
+            Slab &dn = c->slabs[(i + ns - 1) % ns];
+            Slab &up = c->slabs[(i + 1) % ns];
+            const float *p0 = plane0(c, s, cur);
+            // my bottom G planes -> lower neighbour's upper ghosts [nz_dn, nz_dn+G)
+            SQ_HIP(hipMemcpyAsync(plane0(c, dn, cur) + (size_t)dn.nz * plane, p0, gbytes,
+                                  hipMemcpyDeviceToDevice, s.sB));
+            // my top G planes -> upper neighbour's lower ghosts [-G, 0)
+            SQ_HIP(hipMemcpyAsync(up.buf[cur], p0 + (size_t)(s.nz - G) * plane, gbytes,
+                                  hipMemcpyDeviceToDevice, s.sB));
+            SQ_HIP(hipEventRecord(s.evC, s.sB));
+            c->perf.halo_bytes += 2.0 * (double)gbytes;
+        }
+    } else {  // RCCL: one slab per process; this send/recv order pairs correctly for P = 2 too
+        Slab &s = c->slabs[0];
+        float *p0 = plane0(c, s, cur);
+        const int P = c->p.nranks, r = c->p.rank;
+        const int up = (r + 1) % P, dn = (r + P - 1) % P;
+        const size_t n = (size_t)G * plane;
+        SQ_NCCL(ncclGroupStart());
+        SQ_NCCL(ncclSend(p0 + (size_t)(s.nz - G) * plane, n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCL(ncclSend(p0, n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCL(ncclRecv(s.buf[cur], n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCL(ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCL(ncclGroupEnd());
+        SQ_HIP(hipEventRecord(s.evC, s.sB));
+        c->perf.halo_bytes += 2.0 * (double)gbytes;
+    }
+    // 2. step 0, ghost-free core (overlaps the exchange)
+    for (auto &s : c->slabs) {
+        int rc = phi4_launch_span(c, s, cur, s.sA, 1, s.nz - 1, true);
+        if (rc) return rc;
+    }
+    // 3. step 0 rim, after the ghosts arrived and our own sends left
+    for (int i = 0; i < ns; ++i) {
+        Slab &s = c->slabs[i];
+        SQ_HIP(hipStreamWaitEvent(s.sA, s.evC, 0));
+        if (c->p.comm == SQ_COMM_LOOPBACK) {
+            SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
+            SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
+        }
+        const int lo_a = -(g - 1), hi_a = 1, lo_b = s.nz - 1, hi_b = s.nz + g - 1;
+        int rc;
+        if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
+            rc = phi4_launch_span(c, s, cur, s.sA, lo_a, hi_b, false);
+        else
+            rc = phi4_launch_range(c, s, cur, s.sA, lo_a, hi_b, lo_b - lo_a, g, 2, 0, false);
+        if (rc) return rc;
+    }
+    count_step(c);
+    // 4. steps 1..g-1 on the shrinking extended range
+    for (int st = 1; st < g; ++st) {
+        const int in_buf = cur ^ (st & 1);
+        for (auto &s : c->slabs) {
+            int rc = phi4_launch_span(c, s, in_buf, s.sA, -(g - 1 - st), s.nz + (g - 1 - st), true);
+            if (rc) return rc;
+        }
+        count_step(c);
+    }
+    for (auto &s : c->slabs) SQ_HIP(hipEventRecord(s.evA, s.sA));
+    c->cur = cur ^ (g & 1);
+    return SQ_OK;
+}
+
+int phi4_steps(sq_ctx *c, int n) {
+    if (c->p.comm == SQ_COMM_NONE) {
+        for (int i = 0; i < n; ++i) {
+            int rc = phi4_periodic_step(c);
+            if (rc) return rc;
+        }
+        return SQ_OK;
+    }
+    while (n > 0) {
+        const int g = std::min(n, c->gz);
+        int rc = phi4_block(c, g);
+        if (rc) return rc;
+        n -= g;
+    }
     return SQ_OK;
 }
 
@@ -324,24 +390,37 @@ int create_phi4(sq_ctx *c) {
     } else {
         return fail(SQ_E_ARG, "unknown comm");
     }
+    // ghost-zone depth: one exchange of gz planes per gz steps;
+    // bounded by the thinnest slab so a ghost zone never spans two neighbours
+    if (p.comm != SQ_COMM_NONE) {
+        long long nz_min = c->Lz;
+        for (int i = 0; i < nslab; ++i) nz_min = std::min(nz_min, zs[i + 1] - zs[i]);
+        if (p.comm == SQ_COMM_RCCL) nz_min = c->Lz / p.nranks;  // identical on every rank
+        int g = 4;
+        if (const char *e = getenv("SQ_GHOST")) g = std::max(1, atoi(e));
+        c->gz = (int)std::max(1ll, std::min((long long)g, nz_min));
+    }
     const size_t plane = plane_floats(c);
     for (int i = 0; i < nslab; ++i) {
         Slab s;
         s.z0 = zs[i];
         s.nz = (int)(zs[i + 1] - zs[i]);
         if (s.nz < 1) return fail(SQ_E_ARG, "empty slab");
-        const size_t bytes = (size_t)(s.nz + 2) * plane * sizeof(float);
+        const size_t bytes = (size_t)(s.nz + 2 * c->gz) * plane * sizeof(float);
         for (int k = 0; k < 2; ++k) {
             SQ_HIP(hipMalloc(&s.buf[k], bytes));
             SQ_HIP(hipMemset(s.buf[k], 0, bytes));
         }
         SQ_HIP(hipStreamCreateWithFlags(&s.sA, hipStreamNonBlocking));
-        SQ_HIP(hipStreamCreateWithFlags(&s.sB, hipStreamNonBlocking));
+        // halo stream at the highest priority: its RCCL and boundary-plane
+        // kernels must not queue behind the interior kernel's waves
+        int prio_lo = 0, prio_hi = 0;
+        SQ_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        SQ_HIP(hipStreamCreateWithPriority(&s.sB, hipStreamNonBlocking, prio_hi));
         SQ_HIP(hipEventCreateWithFlags(&s.evA, hipEventDisableTiming));
-        SQ_HIP(hipEventCreateWithFlags(&s.evB, hipEventDisableTiming));
-        SQ_HIP(hipEventCreateWithFlags(&s.evPush, hipEventDisableTiming));
+        SQ_HIP(hipEventCreateWithFlags(&s.evC, hipEventDisableTiming));
         SQ_HIP(hipEventRecord(s.evA, s.sA));
-        SQ_HIP(hipEventRecord(s.evB, s.sB));
+        SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->slabs.push_back(s);
     }
     SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
@@ -461,15 +540,13 @@ int phi4_frame(sq_ctx *c, int *stable) {
     for (auto &s : c->slabs) {  // frame-start snapshot, kept on device
         const size_t bytes = (size_t)s.nz * plane * sizeof(float);
         if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
-        SQ_HIP(hipMemcpyAsync(s.snap, s.buf[c->cur] + plane, bytes, hipMemcpyDeviceToDevice, s.sA));
+        SQ_HIP(hipMemcpyAsync(s.snap, plane0(c, s, c->cur), bytes, hipMemcpyDeviceToDevice, s.sA));
     }
     SQ_HIP(hipMemsetAsync(c->flag, 0, sizeof(int), c->slabs[0].sA));
     rc = phi4_join(c);
     if (rc) return rc;
-    for (int j = 0; j < c->p.loops; ++j) {
-        rc = phi4_one_step(c);
-        if (rc) return rc;
-    }
+    rc = phi4_steps(c, c->p.loops);
+    if (rc) return rc;
     rc = phi4_join(c);
     if (rc) return rc;
     Slab &s0 = c->slabs[0];
@@ -483,7 +560,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     if (!*stable) {  // rollback from the device snapshot; the noise counter is NOT rewound,
                      // so a retried frame draws fresh noise (as the reference's LCG state)
         for (auto &s : c->slabs)
-            SQ_HIP(hipMemcpyAsync(s.buf[c->cur] + plane, s.snap, (size_t)s.nz * plane * sizeof(float),
+            SQ_HIP(hipMemcpyAsync(plane0(c, s, c->cur), s.snap, (size_t)s.nz * plane * sizeof(float),
                                   hipMemcpyDeviceToDevice, s.sA));
         rc = phi4_join(c);
         if (rc) return rc;
@@ -570,8 +647,7 @@ int sq_destroy(sq_ctx *c) {
         if (s.sA) (void)hipStreamDestroy(s.sA);
         if (s.sB) (void)hipStreamDestroy(s.sB);
         if (s.evA) (void)hipEventDestroy(s.evA);
-        if (s.evB) (void)hipEventDestroy(s.evB);
-        if (s.evPush) (void)hipEventDestroy(s.evPush);
+        if (s.evC) (void)hipEventDestroy(s.evC);
     }
     for (int k = 0; k < 2; ++k) {
         (void)hipFree(c->qf[k]);
@@ -658,8 +734,8 @@ int sq_step(sq_ctx *c, int nsteps) {
         if (rc) return rc;
         SQ_HIP(hipEventRecord(region->a, c->slabs[0].sA));
     }
-    for (int i = 0; i < nsteps; ++i) {
-        int rc = phi4_one_step(c);
+    {
+        int rc = phi4_steps(c, nsteps);
         if (rc) return rc;
     }
     if (region) {
@@ -707,7 +783,7 @@ int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {
     SQ_HIP(hipDeviceSynchronize());
     size_t off = 0;
     for (auto &s : c->slabs) {
-        SQ_HIP(hipMemcpy(s.buf[c->cur] + plane, phi + off, (size_t)s.nz * plane * sizeof(float),
+        SQ_HIP(hipMemcpy(plane0(c, s, c->cur), phi + off, (size_t)s.nz * plane * sizeof(float),
                          hipMemcpyHostToDevice));
         off += (size_t)s.nz * plane;
     }
@@ -726,7 +802,7 @@ int sq_download_field(sq_ctx *c, float *phi, size_t count) {
     if (rc) return rc;
     size_t off = 0;
     for (auto &s : c->slabs) {
-        SQ_HIP(hipMemcpy(phi + off, s.buf[c->cur] + plane, (size_t)s.nz * plane * sizeof(float),
+        SQ_HIP(hipMemcpy(phi + off, plane0(c, s, c->cur), (size_t)s.nz * plane * sizeof(float),
                          hipMemcpyDeviceToHost));
         off += (size_t)s.nz * plane;
     }
@@ -740,7 +816,7 @@ int sq_init_field(sq_ctx *c, float amp) {
     int rc = phi4_join(c);
     if (rc) return rc;
     for (auto &s : c->slabs)
-        SQ_HIP(sq::phi4_init_launch(s.buf[c->cur], c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
+        SQ_HIP(sq::phi4_init_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
                                     (uint32_t)(c->p.seed >> 32), amp, s.sA));
     return phi4_join(c);
 }
@@ -756,7 +832,7 @@ int sq_moments(sq_ctx *c, double out[3]) {
     for (auto &s : c->slabs) {
         SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));  // same stream as the kernel:
         SQ_HIP(hipMemsetAsync(c->dmax, 0, sizeof(unsigned int), s.sA));  // the null stream does not order non-blocking streams
-        SQ_HIP(sq::phi4_moments_launch(s.buf[c->cur] + plane, (long long)s.nz * (long long)plane,
+        SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane,
                                        c->dacc, c->dmax, s.sA));
         double acc[2];
         unsigned int mx;
@@ -815,7 +891,7 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     double *d = nullptr;
     for (auto &s : c->slabs) {
         SQ_HIP(hipMalloc(&d, sizeof(double) * s.nz));
-        hipError_t e = sq::phi4_slices_launch(s.buf[c->cur], c->Lx, c->Ly, s.nz, d, s.sA);
+        hipError_t e = sq::phi4_slices_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, d, s.sA);
         std::vector<double> h(s.nz);
         if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
         if (e == hipSuccess) e = hipMemcpy(h.data(), d, sizeof(double) * s.nz, hipMemcpyDeviceToHost);

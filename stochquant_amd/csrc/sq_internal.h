@@ -7,18 +7,20 @@
 namespace sq {
 
 // ---------------------------------------------------------------- PHI4 ----
-// One slab lives in a padded buffer of (nz + 2) planes of Lx*Ly floats, z
-// slowest: padded plane 0 is the lower ghost (global z0-1), planes 1..nz the
-// slab, plane nz+1 the upper ghost.  With periodic != 0 the slab is the whole
-// lattice in z and the kernel wraps z itself (ghosts unused).
+// One slab lives in a padded buffer of (nz + 2*gz) planes of Lx*Ly floats, z
+// slowest: padded plane gz + zl holds local plane zl, for zl in [-gz, nz+gz).
+// The gz planes on each side are the ghost zone (deep halo) of the
+// neighbouring slabs.  With periodic != 0 the slab is the whole lattice in z
+// (gz = 1, ghosts unused) and the kernel wraps z itself.
 struct Phi4StepArgs {
     const float *in;
     float *out;
-    int Lx, Ly, nz;
+    int Lx, Ly, nz, gz;
     int zlo, zhi, zstep, zc, nzc;  // chunk k updates planes [zlo + k*zstep, +zc) clipped to zhi
     int periodic;
     int nxseg, nyg, nunits;
     long long zg0;            // global z of local plane 0
+    long long Lzg;            // global Lz (the noise index of ghost-zone planes wraps)
     float h, m2, lam6, sig, clampv;
     uint32_t k0, k1, s_lo, s_hi;
     int *flag;                // guard flag: set to 1 when a site was clamped / NaN (nullable)
@@ -38,13 +40,14 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g);
 // dispatch itself, no extra marker packets on the stream).
 hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s,
                             hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+// slab = local plane 0 (past the ghost zone)
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
 // Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2, acc[2] = max |phi| (as
 // ordered-int bits in acc_max).  acc must be zeroed by the caller.
 hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max,
                                hipStream_t s);
-// Slice sums S(z) = sum_{x,y} phi(x,y,z) for z in [0,nz): out[z] (double).
+// Slice sums S(z) = sum_{x,y} phi(x,y,z) for z in [0,nz): out[z] (double); slab = local plane 0.
 hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double *out,
                               hipStream_t s);
 

@@ -60,7 +60,15 @@ __device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
         if (zl < 0) return A.nz;
         if (zl >= A.nz) return 1;
     }
-    return zl + 1;
+    return zl + A.gz;
+}
+
+// Global z of local plane zl (ghost-zone planes of the first / last slab wrap).
+__device__ __forceinline__ long long global_z(const Phi4StepArgs &A, int zl) {
+    long long zg = A.zg0 + zl;
+    if (zg < 0) zg += A.Lzg;
+    else if (zg >= A.Lzg) zg -= A.Lzg;
+    return zg;
 }
 
 // Guard of tau_kernel.cl:119-133 in two instructions: v_min_f32 returns the
@@ -151,7 +159,7 @@ __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX,
     f32x4n xi[R];
     if constexpr (NZ) {
         u32x4 c[R];
-        const uint32_t qbase = (uint32_t)(A.zg0 + z) * qplane;
+        const uint32_t qbase = (uint32_t)global_z(A, z) * qplane;
 #pragma unroll
         for (int r = 0; r < R; ++r) c[r] = u32x4{qbase + L.qoff[r], kStreamField << 24, A.s_lo, A.s_hi};
         philox_rows<R>(c, A.k0, A.k1);
@@ -164,7 +172,7 @@ __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX,
 #pragma unroll
         for (int r = 0; r < R; ++r) xi[r] = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
-    const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, z + 1, plane, pbytes);
+    const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, A.periodic ? z + 1 : z + A.gz, plane, pbytes);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const float4 cc = C.row[r];
@@ -265,7 +273,7 @@ __global__ __launch_bounds__(256) void phi4_init_kernel(float *slab, int Lx, int
     for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq;
          q += (size_t)gridDim.x * blockDim.x) {
         const f32x4n n = normals4(q0 + q, kStreamInit, 0u, 0u, k0, k1);
-        *reinterpret_cast<float4 *>(slab + plane + 4 * q) = make_float4(amp * n.a, amp * n.b, amp * n.c, amp * n.d);
+        *reinterpret_cast<float4 *>(slab + 4 * q) = make_float4(amp * n.a, amp * n.b, amp * n.c, amp * n.d);
     }
 }
 
@@ -320,7 +328,7 @@ __global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long 
 
 __global__ __launch_bounds__(256) void phi4_slices_kernel(const float *slab, long long plane4,
                                                           double *out) {
-    const float4 *q = reinterpret_cast<const float4 *>(slab) + (size_t)(blockIdx.x + 1) * plane4;
+    const float4 *q = reinterpret_cast<const float4 *>(slab) + (size_t)blockIdx.x * plane4;
     double s = 0;
     for (long long i = threadIdx.x; i < plane4; i += blockDim.x) {
         const float4 v = q[i];

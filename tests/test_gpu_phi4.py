@@ -202,3 +202,39 @@ def test_unsupported_shape_fails_loudly(gpu):
     from stochquant_amd import StochQuantError
     with pytest.raises(StochQuantError):
         _lat((20, 8, 8))
+
+
+@pytest.mark.parametrize("ghost,nslabs,steps", [(1, 2, 5), (2, 3, 7), (4, 2, 9), (4, 4, 8), (8, 2, 13), (3, 5, 4)])
+def test_deep_halo_blocks_bitwise(gpu, oracle_mod, monkeypatch, ghost, nslabs, steps):
+    """Ghost-zone depth G: one exchange per G steps, ghost sites recomputed
+    redundantly; partial blocks when steps % G != 0.  Bit-identical to the
+    single-slab run (counter-based noise makes redundant sites exact)."""
+    shape = (32, 16, 24)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(steps)
+        mono = L.download()
+    monkeypatch.setenv("SQ_GHOST", str(ghost))
+    with _lat(shape, comm="loopback", nslabs=nslabs) as L:
+        L.upload(phi0)
+        for n in (1, steps - 1):
+            L.step(n)
+        assert np.array_equal(mono, L.download())
+
+
+def test_rccl_self_exchange_deep_halo_frames(gpu, oracle_mod, monkeypatch):
+    from stochquant_amd import unique_id
+    shape = (256, 8, 16)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, loops=6) as L:
+        L.upload(phi0)
+        for _ in range(3):
+            assert L.run_frame()
+        mono = L.download()
+    monkeypatch.setenv("SQ_GHOST", "4")
+    with _lat(shape, loops=6, comm="rccl", nranks=1, rank=0, comm_id=unique_id()) as L:
+        L.upload(phi0)
+        for _ in range(3):
+            assert L.run_frame()
+        assert np.array_equal(mono, L.download())
