@@ -371,8 +371,9 @@ int create_phi4(sq_ctx *c) {
         return fail(SQ_E_ARG, "plane exceeds 2 GiB (32-bit buffer offsets)");
     if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
         const int r = atoi(e), rs = 64 / c->geom.qx;
-        if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0) c->geom = sq::Phi4Geom{c->geom.qx, r, rs * r};
+        if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0) c->geom = sq::Phi4Geom{c->geom.qx, r, rs * r, c->geom.pf};
     }
+    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = atoi(e) == 2 ? 2 : 1;
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;

@@ -139,11 +139,10 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several 256-site wave segments (Lx > 256).
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
 template <int QX, int R, bool MS, bool NZ>
-__device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R> &L,
-                                           const Slot<R> &P, const Slot<R> &C, Slot<R> &N, int z,
-                                           int zend, size_t plane, uint32_t pbytes, uint32_t qplane,
-                                           int &bad) {
-    load_slot<QX, R>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+__device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R> &L,
+                                              const Slot<R> &P, const Slot<R> &C, const Slot<R> &N,
+                                              int z, size_t plane, uint32_t pbytes, uint32_t qplane,
+                                              int &bad) {
     float el[R], er[R];
     if constexpr (MS) {
         const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, z), plane, pbytes);
@@ -202,7 +201,28 @@ __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX,
     }
 }
 
+// Prefetch distance 1: load plane z+1 into N, then update plane z.
 template <int QX, int R, bool MS, bool NZ>
+__device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R> &L,
+                                           const Slot<R> &P, const Slot<R> &C, Slot<R> &N, int z,
+                                           int zend, size_t plane, uint32_t pbytes, uint32_t qplane,
+                                           int &bad) {
+    load_slot<QX, R>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+    plane_compute<QX, R, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+}
+
+// Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
+// whole plane of work ahead of its use), then update plane z.
+template <int QX, int R, bool MS, bool NZ>
+__device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX, R> &L,
+                                            const Slot<R> &P, const Slot<R> &C, const Slot<R> &N,
+                                            Slot<R> &F, int z, int zend, size_t plane, uint32_t pbytes,
+                                            uint32_t qplane, int &bad) {
+    if (z + 2 <= zend) load_slot<QX, R>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
+    plane_compute<QX, R, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+}
+
+template <int QX, int R, bool MS, bool NZ, int PF>
 __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     constexpr int RS = 64 / QX;  // row sets per wave
     const int nb = gridDim.x, b = blockIdx.x;
@@ -250,13 +270,28 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     load_slot<QX, R>(A, L, S0, zbeg - 1, false, plane, pbytes);
     load_slot<QX, R>(A, L, S1, zbeg, true, plane, pbytes);
     int bad = 0;
-    // three-slot register queue, unrolled so no rotation moves are needed
-    for (int z = zbeg; z < zend; z += 3) {
-        plane_step<QX, R, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
-        if (z + 1 >= zend) break;
-        plane_step<QX, R, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
-        if (z + 2 >= zend) break;
-        plane_step<QX, R, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+    if constexpr (PF == 1) {
+        // three-slot register queue, unrolled so no rotation moves are needed
+        for (int z = zbeg; z < zend; z += 3) {
+            plane_step<QX, R, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            if (z + 1 >= zend) break;
+            plane_step<QX, R, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            if (z + 2 >= zend) break;
+            plane_step<QX, R, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+        }
+    } else {
+        // four-slot queue, prefetch distance 2
+        Slot<R> S3;
+        load_slot<QX, R>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
+        for (int z = zbeg; z < zend; z += 4) {
+            plane_step2<QX, R, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, bad);
+            if (z + 1 >= zend) break;
+            plane_step2<QX, R, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            if (z + 2 >= zend) break;
+            plane_step2<QX, R, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            if (z + 3 >= zend) break;
+            plane_step2<QX, R, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, bad);
+        }
     }
     if (!L.rows_ok) bad = 0;
     if (A.flag != nullptr) {
@@ -357,13 +392,13 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     const int rcand[3] = {one_seg ? 1 : 2, one_seg ? 2 : 4, one_seg ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
         if (Ly % (rs * r) == 0) {
-            *g = Phi4Geom{qx, r, rs * r};
+            *g = Phi4Geom{qx, r, rs * r, 1};
             return true;
         }
     }
     for (int r : rcand) {  // otherwise a partial last tile (rows past Ly idle)
         if (Ly % r == 0) {
-            *g = Phi4Geom{qx, r, rs * r};
+            *g = Phi4Geom{qx, r, rs * r, 1};
             return true;
         }
     }
@@ -376,30 +411,38 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g) {
     a.nunits = a.nxseg * a.nyg * a.nzc;
 }
 
-template <int QX, int R, bool MS, bool NZ>
-static hipError_t launch_nz(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
+template <int QX, int R, bool MS, bool NZ, int PF>
+static hipError_t launch_pf(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
                             hipEvent_t e1) {
     if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ>), grid, dim3(256), 0, s, e0, e1, 0, a);
+        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ, PF>), grid, dim3(256), 0, s, e0, e1, 0, a);
     else
-        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ, PF>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
+template <int QX, int R, bool MS, bool NZ>
+static hipError_t launch_nz(const Phi4StepArgs &a, int pf, dim3 grid, hipStream_t s, hipEvent_t e0,
+                            hipEvent_t e1) {
+    if constexpr (QX == 64)  // the deeper queue is only built for full-row waves
+        if (pf == 2) return launch_pf<QX, R, MS, NZ, 2>(a, grid, s, e0, e1);
+    return launch_pf<QX, R, MS, NZ, 1>(a, grid, s, e0, e1);
+}
+
 template <int QX, int R, bool MS>
-static hipError_t launch_one(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
+static hipError_t launch_one(const Phi4StepArgs &a, int pf, dim3 grid, hipStream_t s, hipEvent_t e0,
                              hipEvent_t e1) {
-    return a.sig != 0.0f ? launch_nz<QX, R, MS, true>(a, grid, s, e0, e1)
-                         : launch_nz<QX, R, MS, false>(a, grid, s, e0, e1);
+    return a.sig != 0.0f ? launch_nz<QX, R, MS, true>(a, pf, grid, s, e0, e1)
+                         : launch_nz<QX, R, MS, false>(a, pf, grid, s, e0, e1);
 }
 
 template <int QX, bool MS>
-static hipError_t launch_qx(const Phi4StepArgs &a, int r, dim3 grid, hipStream_t s, hipEvent_t e0,
-                            hipEvent_t e1) {
+static hipError_t launch_qx(const Phi4StepArgs &a, int r, int pf, dim3 grid, hipStream_t s,
+                            hipEvent_t e0, hipEvent_t e1) {
     switch (r) {
-    case 4: return launch_one<QX, 4, MS>(a, grid, s, e0, e1);
-    case 2: return launch_one<QX, 2, MS>(a, grid, s, e0, e1);
-    default: return launch_one<QX, 1, MS>(a, grid, s, e0, e1);
+    case 4: return launch_one<QX, 4, MS>(a, pf, grid, s, e0, e1);
+    case 2: return launch_one<QX, 2, MS>(a, pf, grid, s, e0, e1);
+    default: return launch_one<QX, 1, MS>(a, pf, grid, s, e0, e1);
     }
 }
 
@@ -409,13 +452,13 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
     const dim3 grid((unsigned)((a.nunits + 3) / 4));
     switch (g.qx) {
     case 64:
-        return a.nxseg > 1 ? launch_qx<64, true>(a, g.r, grid, s, e0, e1)
-                           : launch_qx<64, false>(a, g.r, grid, s, e0, e1);
-    case 32: return launch_qx<32, false>(a, g.r, grid, s, e0, e1);
-    case 16: return launch_qx<16, false>(a, g.r, grid, s, e0, e1);
-    case 8: return launch_qx<8, false>(a, g.r, grid, s, e0, e1);
-    case 4: return launch_qx<4, false>(a, g.r, grid, s, e0, e1);
-    case 2: return launch_qx<2, false>(a, g.r, grid, s, e0, e1);
+        return a.nxseg > 1 ? launch_qx<64, true>(a, g.r, g.pf, grid, s, e0, e1)
+                           : launch_qx<64, false>(a, g.r, g.pf, grid, s, e0, e1);
+    case 32: return launch_qx<32, false>(a, g.r, g.pf, grid, s, e0, e1);
+    case 16: return launch_qx<16, false>(a, g.r, g.pf, grid, s, e0, e1);
+    case 8: return launch_qx<8, false>(a, g.r, g.pf, grid, s, e0, e1);
+    case 4: return launch_qx<4, false>(a, g.r, g.pf, grid, s, e0, e1);
+    case 2: return launch_qx<2, false>(a, g.r, g.pf, grid, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
 }

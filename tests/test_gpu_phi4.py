@@ -238,3 +238,15 @@ def test_rccl_self_exchange_deep_halo_frames(gpu, oracle_mod, monkeypatch):
         for _ in range(3):
             assert L.run_frame()
         assert np.array_equal(mono, L.download())
+
+
+@pytest.mark.parametrize("shape", [(256, 8, 8), (256, 4, 33), (512, 4, 6), (256, 16, 5)])
+@pytest.mark.parametrize("pf", [1, 2])
+def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
+    monkeypatch.setenv("SQ_PREFETCH", str(pf))
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, C=0.0) as L:
+        L.upload(phi0)
+        L.step(3)
+        got = L.download()
+    assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
