@@ -442,7 +442,9 @@ int create_phi4(sq_ctx *c) {
     // enough to give >= ~8 waves per CU.
     const long long rows = (long long)(c->Lx / (4 * c->geom.qx)) * (c->Ly / c->geom.wy);
     const int nz_max = c->slabs[0].nz;
-    int zc = 4;  // measured optimum at 256^3 and 512^3 (profiles/r01/sweep*)
+    // measured optima (profiles/r01/sweep*): zc = 4 for one-segment rows (256^3),
+    // zc = 8 when rows span several 256-site segments (512^3)
+    int zc = c->Lx > 256 ? 8 : 4;
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     c->zc = zc;
