@@ -92,6 +92,7 @@ struct sq_ctx {
     double *qf[2] = {nullptr, nullptr}, *qx[2] = {nullptr, nullptr}, *qxx0[2] = {nullptr, nullptr};
     int qcur = 0;
     sq::Qm1dState *qst = nullptr;
+    double *qscr[3] = {nullptr, nullptr, nullptr};  // N > 8192: fs, xs, ds of Qm1dArgs
     double omega = 0;
     long runs = 0;
     int lrgEl = 0;
@@ -457,7 +458,7 @@ int create_qm1d(sq_ctx *c) {
     if (p.dims[0] < 2 || p.dims[0] > (1 << 30)) return fail(SQ_E_ARG, "QM1D needs N >= 2");
     c->N = (int)p.dims[0];
     if (sq::qm1d_sites_per_thread(c->N) == 0)
-        return fail(SQ_E_ARG, "QM1D single-workgroup kernel supports N <= 8192");
+        return fail(SQ_E_ARG, "QM1D supports 2 <= N <= 65536 (one work-group per frame)");
     if (p.pot != 0 && p.pot != 3) return fail(SQ_E_ARG, "potID must be 0 or 3 (tau_kernel.cl:215-246)");
     if (!(p.deltat > 0)) return fail(SQ_E_ARG, "deltat must be > 0");
     if (p.loops < 1) return fail(SQ_E_ARG, "loops must be >= 1");
@@ -470,6 +471,8 @@ int create_qm1d(sq_ctx *c) {
         SQ_HIP(hipMemset(c->qx[k], 0, bytes));
         SQ_HIP(hipMemset(c->qxx0[k], 0, bytes));
     }
+    if (sq::qm1d_sites_per_thread(c->N) > 8)  // global-memory variant: f ping-pong + scan scratch
+        for (double **q : {&c->qscr[0], &c->qscr[1], &c->qscr[2]}) SQ_HIP(hipMalloc(q, bytes));
     SQ_HIP(hipMalloc(&c->qst, sizeof(sq::Qm1dState)));
     SQ_HIP(hipStreamCreateWithFlags(&c->qstream, hipStreamNonBlocking));
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
@@ -485,6 +488,9 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     a.nf = c->qf[k ^ 1];
     a.nx = c->qx[k ^ 1];
     a.nxx0 = c->qxx0[k ^ 1];
+    a.fs = c->qscr[0];
+    a.xs = c->qscr[1];
+    a.ds = c->qscr[2];
     a.st = c->qst;
     a.N = c->N;
     a.pot = c->p.pot;
@@ -662,6 +668,7 @@ int sq_destroy(sq_ctx *c) {
         (void)hipFree(c->qxx0[k]);
     }
     (void)hipFree(c->qst);
+    for (double *q : c->qscr) (void)hipFree(q);
     (void)hipFree(c->flag);
     (void)hipFree(c->dacc);
     (void)hipFree(c->dmax);

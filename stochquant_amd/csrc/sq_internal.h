@@ -66,6 +66,7 @@ struct Qm1dState {    // device-resident frame scalars
 struct Qm1dArgs {
     const double *f, *x, *xx0;  // frame-start state (N)
     double *nf, *nx, *nxx0;     // state after the frame (N)
+    double *fs, *xs, *ds;       // N > 8192 only: f ping-pong, X' and drift-check scratch (N each)
     Qm1dState *st;
     int N, pot, loops, runs;
     double a, a2, h, sig, sigw, kconst;
@@ -73,7 +74,8 @@ struct Qm1dArgs {
     unsigned long long tick;    // Philox step index of the frame's first step
 };
 
-int qm1d_sites_per_thread(int N);  // 0 if N unsupported
+int qm1d_sites_per_thread(int N);  // 0 if N unsupported; > 8 = global-memory variant
+constexpr int kQm1dMaxN = 1024 * 64;
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
 
 // -------------------------------------------------------------- selftest --

@@ -226,11 +226,152 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs 
     }
 }
 
+// The same frame for N > 8192 (config C1's 32,768-site chain): one work-group,
+// K sites per thread held in global memory (L2-resident at these sizes)
+// instead of registers.  Every thread reads and writes only its own sites;
+// neighbour edges and f[mid] still go through LDS, so no cross-thread global
+// visibility is needed.  f ping-pongs between nf and the scratch fs (the
+// frame-start f stays untouched: it is the rollback snapshot); X' and the
+// drift check of each site are parked in scratch for the scan walk.
+template <int K>
+__global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1dArgs A) {
+    __shared__ double s_first[kMaxThreads], s_last[kMaxThreads];
+    __shared__ double s_wmaxX[kMaxThreads / 64], s_wmaxA[kMaxThreads / 64];
+    __shared__ double s_fmid, s_R;
+    __shared__ int s_leader[2];
+
+    const int N = A.N, pot = A.pot, mid = N / 2;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
+    const int i0 = t * K;
+    const int own = max(0, min(K, N - i0));
+    const double h = A.h, a = A.a, a2 = A.a2;
+    for (int k = 0; k < own; ++k) {
+        A.nx[i0 + k] = A.x[i0 + k];
+        A.nxx0[i0 + k] = A.xx0[i0 + k];
+    }
+    double om = A.st->omega_in;
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int stable = 1, steps = 0;
+    const double *fin = A.f;
+    double *fout = A.nf;
+
+    for (int j = 0; j < A.loops; ++j) {
+        const unsigned long long step = A.tick + (unsigned long long)j;
+        const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
+        s_first[t] = own ? fin[i0] : 0.;
+        s_last[t] = own ? fin[i0 + own - 1] : 0.;
+        if (mid >= i0 && mid < i0 + own) s_fmid = fin[mid];
+        if (t == 0) s_leader[j & 1] = -1;
+        __syncthreads();
+        const double fL = t > 0 ? s_last[t - 1] : 0.;
+        const double fR = (t + 1 < (int)blockDim.x) ? s_first[t + 1] : 0.;
+        const double Xm = s_fmid + xcl((double)mid * a, om, pot);
+        const double den = (double)(A.runs + j + 1);
+        double prev_old = fL;
+        double lmaxX = -INFINITY, lmaxA = -INFINITY;
+        f32x4n nq{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < own; ++k) {
+            const int i = i0 + k;
+            if ((k & 3) == 0)
+                nq = normals4((unsigned long long)(i >> 2), kStreamField, slo, shi, A.k0, A.k1);
+            const float xi = (k & 3) == 0 ? nq.a : (k & 3) == 1 ? nq.b : (k & 3) == 2 ? nq.c : nq.d;
+            const double fi = fin[i];
+            const double fr = (k + 1 < own) ? fin[i + 1] : fR;
+            const double xc = xcl((double)i * a, om, pot);
+            const double dw = A.sig * (double)xi;
+            double v;
+            if (i == 0)
+                v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
+                    ddpot(xc, pot) * fi * h + dw;
+            else if (i == N - 1)
+                v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
+                    ddpot(xc, pot) * fi * h + dw;
+            else
+                v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
+            if (v > 1000) v = 1000;
+            if (v < -1000) v = -1000;
+            if (v != v) v = 1000;
+            const double X = v + xc;
+            A.xs[i] = X;
+            A.ds[i] = absol(v - fi - dw);
+            lmaxX = fmax(lmaxX, X);
+            lmaxA = fmax(lmaxA, absol(X));
+            const double Xi = fi + xc;
+            A.nxx0[i] = A.nxx0[i] + (Xi * Xm - A.nxx0[i]) / den;
+            A.nx[i] = A.nx[i] + (Xi - A.nx[i]) / den;
+            prev_old = fi;
+            fout[i] = v;
+        }
+        if (E >= i0 && E < i0 + own) s_R = A.xs[E];
+        const double ix = wave_incl_max(lmaxX, lane);
+        const double ia = wave_incl_max(lmaxA, lane);
+        double ex = __shfl_up(ix, 1, 64), ea = __shfl_up(ia, 1, 64);
+        if (lane == 0) {
+            ex = -INFINITY;
+            ea = -INFINITY;
+        }
+        if (lane == 63) {
+            s_wmaxX[wv] = ix;
+            s_wmaxA[wv] = ia;
+        }
+        __syncthreads();
+        double runX = s_R, runA = V, totA = V;
+        for (int w = 0; w < nw; ++w) {
+            const double wx = s_wmaxX[w], wa = s_wmaxA[w];
+            if (w < wv) {
+                runX = fmax(runX, wx);
+                runA = fmax(runA, wa);
+            }
+            totA = fmax(totA, wa);
+        }
+        runX = fmax(runX, ex);
+        runA = fmax(runA, ea);
+        int unst = 0, leader = -1;
+        for (int k = 0; k < own; ++k) {
+            const int i = i0 + k;
+            const double X = A.xs[i];
+            if (X > runX) {
+                runX = X;
+                leader = i;
+                if (A.ds[i] > runA) unst = 1;
+            }
+            runA = fmax(runA, absol(X));
+        }
+        if (leader >= 0) atomicMax(&s_leader[j & 1], leader);
+        const int any_unst = __syncthreads_or(unst);
+        const int Lw = s_leader[j & 1];
+        if (Lw >= 0) E = Lw;
+        V = totA;
+        const f32x4n nwn = normals4(0ull, kStreamOmega, slo, shi, A.k0, A.k1);
+        const double nwo = om + A.kconst * (A.sigw * (double)nwn.a);
+        if (nwo > (double)(N - 1) * a) om = 2 * (double)(N - 1) * a - nwo;
+        else if (nwo < 0) om = -nwo;
+        else om = nwo;
+        steps = j + 1;
+        fin = fout;
+        fout = (fout == A.nf) ? A.fs : A.nf;
+        if (any_unst) {
+            stable = 0;
+            break;
+        }
+    }
+    if (fin != A.nf)
+        for (int k = 0; k < own; ++k) A.nf[i0 + k] = fin[i0 + k];
+    if (t == 0) {
+        A.st->omega_out = om;
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = stable;
+        A.st->steps_done = steps;
+    }
+}
+
 }  // namespace
 
 int qm1d_sites_per_thread(int N) {
-    if (N < 2) return 0;
-    for (int k : {1, 2, 4, 8})
+    if (N < 2 || N > kQm1dMaxN) return 0;
+    for (int k : {1, 2, 4, 8, 16, 32, 64})
         if ((N + k - 1) / k <= kMaxThreads) return k;
     return 0;
 }
@@ -244,7 +385,10 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
     case 1: hipLaunchKernelGGL(qm1d_frame_kernel<1>, dim3(1), dim3(threads), 0, s, a); break;
     case 2: hipLaunchKernelGGL(qm1d_frame_kernel<2>, dim3(1), dim3(threads), 0, s, a); break;
     case 4: hipLaunchKernelGGL(qm1d_frame_kernel<4>, dim3(1), dim3(threads), 0, s, a); break;
-    default: hipLaunchKernelGGL(qm1d_frame_kernel<8>, dim3(1), dim3(threads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(qm1d_frame_kernel<8>, dim3(1), dim3(threads), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(qm1d_frame_kernel_glob<16>, dim3(1), dim3(threads), 0, s, a); break;
+    case 32: hipLaunchKernelGGL(qm1d_frame_kernel_glob<32>, dim3(1), dim3(threads), 0, s, a); break;
+    default: hipLaunchKernelGGL(qm1d_frame_kernel_glob<64>, dim3(1), dim3(threads), 0, s, a); break;
     }
     return hipGetLastError();
 }

@@ -156,3 +156,30 @@ def test_sampled_covariance_matches_exact_jacobi_law(gpu):
         m, err = b.mean(), b.std(ddof=1) / np.sqrt(len(b))
         print(j, m, "+-", err, "exact", exact[j, mid])
         assert abs(m - exact[j, mid]) < 4 * err + 0.01
+
+
+@pytest.mark.parametrize("N", [8193, 16384, 32768, 65536])
+def test_large_chain_noiseless_frame_bitwise(gpu, oracle_mod, N):
+    """N > 8192: the global-memory single-work-group variant, same semantics."""
+    a, h, loops = 0.1, 0.002, 30
+    f, x, xx0 = _state(N)
+    om = N * a / 2
+    stable, d, sc = _gpu_frame(N, a, h, 0, 0.0, loops, 9, f, x, xx0, om, runs=7, lrgVl=0.3)
+    r = oracle_mod.qm1d_frame(N, a, h, 0, 0.0, loops, 9, 0, 7, f, x, xx0, om, 0, 0.3)
+    assert stable == (r["stable"] == 1) and stable
+    for k in ("f", "x", "xx0"):
+        assert np.array_equal(d[k], r[k])
+    assert d["omega"] == r["omega"] and sc["lrgEl"] == r["lrgEl"] and sc["lrgVl"] == r["lrgVl"]
+
+
+def test_large_chain_double_well_within_tolerance(gpu, oracle_mod):
+    N, a, h, loops = 32768, 0.1, 0.002, 20
+    f, x, xx0 = _state(N)
+    om = N * a / 2 + 0.013
+    stable, d, sc = _gpu_frame(N, a, h, 3, 1.0, loops, 21, f, x, xx0, om, runs=3, lrgVl=1.0)
+    r = oracle_mod.qm1d_frame(N, a, h, 3, 1.0, loops, 21, 0, 3, f, x, xx0, om, 0, 1.0)
+    assert r["stable"] == 1 and stable
+    sig = np.sqrt(np.float32(2 * h / a))
+    tol = loops * (sig * 1.4e-5 + 2e-6)
+    for k in ("f", "x", "xx0"):
+        assert np.max(np.abs(d[k] - r[k])) <= tol

@@ -83,3 +83,21 @@ def test_plotted_correlator_matches_exact_stationary_value(gpu, tmp_path):
     exact = stationary_cov(100, 0.1, 0.002, "jacobi")[40:60, 50]
     assert np.all(np.isfinite(c))
     assert abs(c.mean() - exact.mean()) < 0.3 * exact.mean()
+
+
+def test_config_c1_chain_through_tauhost(gpu, tmp_path):
+    """BASELINE configs[0] / SURVEY §8d C1: the "32^3" chain = N = 32,768 sites,
+    dt = 1, dtau = 0.01, potID 0, C = 1, 1000 steps, fresh start, via the
+    drop-in executable.  The bulk <f^2> relaxes to the exact Euler-Maruyama
+    value 0.29378 (tests/golden/analytic_kats.json; the survey's serial oracle
+    run gave 0.2943)."""
+    g = golden("analytic_kats.json")["free_var_1d"]
+    argv = ["32768", "1.0", "0.01", "1", "0", "1", "0", "1", "0", "1000", "0", "END", "17"]
+    out, end = _run(tmp_path, argv)
+    lines = end.strip().split("\n")
+    f = np.array([float.fromhex(ln.split("|")[3].strip()) for ln in lines[:32768]])
+    bulk = f[256:-256]
+    m2 = np.mean(bulk ** 2)
+    err = 2 * np.std(bulk ** 2) / np.sqrt(bulk.size) * 3   # ~3 sites correlation length
+    assert abs(m2 - g["value"]) < 4 * err
+    assert lines[-2].strip() == "1000|N"
