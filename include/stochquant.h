@@ -113,8 +113,8 @@ int sq_init_field(sq_ctx *ctx, float amp);
 /* PHI4 local slab geometry: nz_local and the global z of its first plane. */
 int sq_slab(sq_ctx *ctx, long long *nz_local, long long *z0);
 /* PHI4 register tile of the step kernel: out = {lanes per x segment, rows
- * per lane, z planes per wave}. */
-int sq_phi4_tile(sq_ctx *ctx, int out[3]);
+ * per lane, z planes per wave, float4 segments per lane per row}. */
+int sq_phi4_tile(sq_ctx *ctx, int out[4]);
 /* PHI4 observables over this process' slab: out[0] = sum phi, out[1] = sum
  * phi^2, out[2] = max |phi| (double accumulation on device). */
 int sq_moments(sq_ctx *ctx, double out[3]);

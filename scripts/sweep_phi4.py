@@ -23,16 +23,21 @@ def main():
     ap.add_argument("--rows", default="1,2,4")
     ap.add_argument("--zc", default="2,4,8,16")
     ap.add_argument("--pf", default="1", help="z prefetch distances to try (1,2)")
+    ap.add_argument("--vseg", default="0", help="float4 segments per lane to try (0 = library default)")
     ap.add_argument("--C", type=float, default=1.0, help="noise amplitude (0: RNG-free gradient-flow kernel)")
     a = ap.parse_args()
     from stochquant_amd import Phi4Lattice
     L = a.size
     variants = list(itertools.product([int(r) for r in a.rows.split(",")], [int(z) for z in a.zc.split(",")],
-                                      [int(p) for p in a.pf.split(",")]))
+                                      [int(p) for p in a.pf.split(",")], [int(v) for v in a.vseg.split(",")]))
     res = {v: [] for v in variants}
     lats = {}
     for v in variants:
         os.environ["SQ_ROWS"], os.environ["SQ_ZCHUNK"], os.environ["SQ_PREFETCH"] = str(v[0]), str(v[1]), str(v[2])
+        if v[3]:
+            os.environ["SQ_VSEG"] = str(v[3])
+        else:
+            os.environ.pop("SQ_VSEG", None)
         lat = Phi4Lattice((L, L, L), dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, C=a.C)
         lat.init_field(0.1)
         lat.step(50)
@@ -41,7 +46,7 @@ def main():
     for rnd in range(a.rounds):
         for v in variants:
             lat = lats[v]
-            row = {"rows": v[0], "zc": v[1], "pf": v[2], "round": rnd}
+            row = {"rows": v[0], "zc": v[1], "pf": v[2], "vseg": v[3], "round": rnd}
             for mode in (0, 1, 2):
                 lat.perf_reset()
                 lat.set_profiling(mode)
@@ -61,7 +66,7 @@ def main():
     for v in sorted(variants, key=lambda v: statistics.median(k for k, _ in res[v])):
         k = statistics.median(x for x, _ in res[v])
         w = statistics.median(y for _, y in res[v])
-        print(f"rows={v[0]} zc={v[1]:3d} pf={v[2]}  kernel {k:8.3f} us  wall {w:8.3f} us  {8 * L ** 3 / (k * 1e-6) / 1e9:8.1f} GB/s")
+        print(f"rows={v[0]} zc={v[1]:3d} pf={v[2]} v={v[3]}  kernel {k:8.3f} us  wall {w:8.3f} us  {8 * L ** 3 / (k * 1e-6) / 1e9:8.1f} GB/s")
     for lat in lats.values():
         lat.close()
 

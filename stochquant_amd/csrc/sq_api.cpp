@@ -372,8 +372,11 @@ int create_phi4(sq_ctx *c) {
         return fail(SQ_E_ARG, "plane exceeds 2 GiB (32-bit buffer offsets)");
     if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
         const int r = atoi(e), rs = 64 / c->geom.qx;
-        if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0) c->geom = sq::Phi4Geom{c->geom.qx, r, rs * r, c->geom.pf};
+        if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0)
+            c->geom = sq::Phi4Geom{c->geom.qx, r, rs * r, c->geom.pf, c->geom.v};
     }
+    if (const char *e = getenv("SQ_VSEG"))  // tuning override: float4 segments per lane
+        if (atoi(e) == 1 || (atoi(e) == 2 && c->geom.qx == 64 && c->Lx % 512 == 0)) c->geom.v = atoi(e);
     if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = atoi(e) == 2 ? 2 : 1;
     int nslab = 1;
     long long zfirst = 0;
@@ -441,11 +444,11 @@ int create_phi4(sq_ctx *c) {
     }
     // z chunk per wave: long enough to amortise the chunk-edge planes, short
     // enough to give >= ~8 waves per CU.
-    const long long rows = (long long)(c->Lx / (4 * c->geom.qx)) * (c->Ly / c->geom.wy);
+    const long long rows = (long long)(c->Lx / (4 * c->geom.qx * c->geom.v)) * (c->Ly / c->geom.wy);
     const int nz_max = c->slabs[0].nz;
     // measured optima (profiles/r01/sweep*): zc = 4 for one-segment rows (256^3),
     // zc = 8 when rows span several 256-site segments (512^3)
-    int zc = c->Lx > 256 ? 8 : 4;
+    int zc = c->Lx > 4 * c->geom.qx * c->geom.v ? 8 : 4;
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     c->zc = zc;
@@ -777,12 +780,13 @@ int sq_slab(sq_ctx *c, long long *nz_local, long long *z0) {
     return SQ_OK;
 }
 
-int sq_phi4_tile(sq_ctx *c, int out[3]) {
+int sq_phi4_tile(sq_ctx *c, int out[4]) {
     if (!c || !out) return fail(SQ_E_ARG, "null argument");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
     out[0] = c->geom.qx;
     out[1] = c->geom.r;
     out[2] = c->zc;
+    out[3] = c->geom.v;
     return SQ_OK;
 }
 

@@ -30,7 +30,8 @@ struct Phi4Geom {
     int qx;   // lanes per x segment (4 sites each)
     int r;    // rows per lane
     int wy;   // rows per wave unit
-    int pf;   // z prefetch distance of the register queue (1 or 2; 2 only for qx == 64)
+    int pf;   // z prefetch distance of the register queue (1 or 2; 2 only for qx == 64, v == 1)
+    int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 
 // Picks the register tile for (Lx, Ly); returns false if unsupported.

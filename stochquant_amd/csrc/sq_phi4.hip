@@ -107,42 +107,49 @@ __device__ __forceinline__ void philox_rows(u32x4 (&c)[R], uint32_t k0, uint32_t
     }
 }
 
-template <int R>
+// A lane holds, per row, V float4 of the wave's x-span: segment v at
+// x = x0 + 256 v + 4 lane (each load is still one contiguous 1-KiB wave access).
+template <int R, int V>
 struct Slot {
-    float4 row[R];
-    float4 hm, hp;  // y-halo rows of the same plane
+    float4 row[R * V];   // index r*V + v
+    float4 hm[V], hp[V]; // y-halo rows of the same plane
 };
 
-template <int QX, int R>
+template <int QX, int R, int V>
 struct Lane {
-    uint32_t voff[R];       // byte offset of the lane's float4 in each of its rows
-    uint32_t vm, vp;        // halo rows
-    uint32_t vl[R], vr[R];  // x-1 / x+4 neighbours across segment edges (multiseg)
-    uint32_t qoff[R];       // Philox quad offset inside the plane
+    uint32_t voff[R * V];   // byte offset of each float4 inside the plane
+    uint32_t vm[V], vp[V];  // halo rows
+    uint32_t vl[R], vr[R];  // x-1 of the span's first site / x+1 of its last (MS only)
+    uint32_t qoff[R * V];   // Philox quad offset inside the plane
     bool rows_ok;
     int lane;
 };
 
-template <int QX, int R>
-__device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, R> &L, Slot<R> &s,
-                                          int zl, bool halo, size_t plane, uint32_t pbytes) {
+template <int QX, int R, int V>
+__device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
+                                          Slot<R, V> &s, int zl, bool halo, size_t plane,
+                                          uint32_t pbytes) {
     const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, zl), plane, pbytes);
 #pragma unroll
-    for (int r = 0; r < R; ++r) s.row[r] = bload4(rs, L.voff[r]);
+    for (int k = 0; k < R * V; ++k) s.row[k] = bload4(rs, L.voff[k]);
     if (halo) {
-        s.hm = bload4(rs, L.vm);
-        s.hp = bload4(rs, L.vp);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            s.hm[v] = bload4(rs, L.vm[v]);
+            s.hp[v] = bload4(rs, L.vp[v]);
+        }
     }
 }
 
-// Update plane z from slots P (z-1), C (z), N (z+1); N is loaded here first.
-// MS: the row spans several 256-site wave segments (Lx > 256).
+// Update plane z from slots P (z-1), C (z), N (z+1).
+// MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
+//     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, bool MS, bool NZ>
-__device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R> &L,
-                                              const Slot<R> &P, const Slot<R> &C, const Slot<R> &N,
-                                              int z, size_t plane, uint32_t pbytes, uint32_t qplane,
-                                              int &bad) {
+template <int QX, int R, int V, bool MS, bool NZ>
+__device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
+                                              const Slot<R, V> &P, const Slot<R, V> &C,
+                                              const Slot<R, V> &N, int z, size_t plane,
+                                              uint32_t pbytes, uint32_t qplane, int &bad) {
     float el[R], er[R];
     if constexpr (MS) {
         const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, z), plane, pbytes);
@@ -154,75 +161,90 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
             if (L.lane == 63) er[r] = bload1(rs, L.vr[r]);
         }
     }
-    // noise for the R float4s of plane z: independent of the loads in flight
-    f32x4n xi[R];
+    // noise for the R*V float4s of plane z: independent of the loads in flight
+    f32x4n xi[R * V];
     if constexpr (NZ) {
-        u32x4 c[R];
+        u32x4 c[R * V];
         const uint32_t qbase = (uint32_t)global_z(A, z) * qplane;
 #pragma unroll
-        for (int r = 0; r < R; ++r) c[r] = u32x4{qbase + L.qoff[r], kStreamField << 24, A.s_lo, A.s_hi};
-        philox_rows<R>(c, A.k0, A.k1);
+        for (int k = 0; k < R * V; ++k) c[k] = u32x4{qbase + L.qoff[k], kStreamField << 24, A.s_lo, A.s_hi};
+        philox_rows<R * V>(c, A.k0, A.k1);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            box_muller(c[r].x, c[r].y, xi[r].a, xi[r].b);
-            box_muller(c[r].z, c[r].w, xi[r].c, xi[r].d);
+        for (int k = 0; k < R * V; ++k) {
+            box_muller(c[k].x, c[k].y, xi[k].a, xi[k].b);
+            box_muller(c[k].z, c[k].w, xi[k].c, xi[k].d);
         }
     } else {
 #pragma unroll
-        for (int r = 0; r < R; ++r) xi[r] = f32x4n{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < R * V; ++k) xi[k] = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
     const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, A.periodic ? z + 1 : z + A.gz, plane, pbytes);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const float4 cc = C.row[r];
-        const float4 up = r > 0 ? C.row[r > 0 ? r - 1 : 0] : C.hm;
-        const float4 dn = r < R - 1 ? C.row[r < R - 1 ? r + 1 : 0] : C.hp;
-        float lft, rgt;
-        if constexpr (QX == 64) {
-            lft = from_left_lane(cc.w);
-            rgt = from_right_lane(cc.x);
-        } else {
-            const int seg = L.lane & ~(QX - 1), xq = L.lane & (QX - 1);
-            lft = __shfl(cc.w, seg | ((xq + QX - 1) & (QX - 1)), 64);
-            rgt = __shfl(cc.x, seg | ((xq + 1) & (QX - 1)), 64);
+        // x-neighbours across lanes: rotate every segment's edge element once,
+        // then lane 0 / 63 take the value rotated out of the adjacent segment
+        float rl[V], rr[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const float4 cc = C.row[r * V + v];
+            if constexpr (QX == 64) {
+                rl[v] = from_left_lane(cc.w);
+                rr[v] = from_right_lane(cc.x);
+            } else {
+                const int seg = L.lane & ~(QX - 1), xq = L.lane & (QX - 1);
+                rl[v] = __shfl(cc.w, seg | ((xq + QX - 1) & (QX - 1)), 64);
+                rr[v] = __shfl(cc.x, seg | ((xq + 1) & (QX - 1)), 64);
+            }
         }
-        if constexpr (MS) {
-            if (L.lane == 0) lft = el[r];
-            if (L.lane == 63) rgt = er[r];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int k = r * V + v;
+            const float4 cc = C.row[k];
+            const float4 up = r > 0 ? C.row[r > 0 ? k - V : 0] : C.hm[v];
+            const float4 dn = r < R - 1 ? C.row[r < R - 1 ? k + V : 0] : C.hp[v];
+            float lft = rl[v], rgt = rr[v];
+            if constexpr (V > 1) {
+                if (L.lane == 0) lft = rl[(v + V - 1) % V];
+                if (L.lane == 63) rgt = rr[(v + 1) % V];
+            }
+            if constexpr (MS) {
+                if (v == 0 && L.lane == 0) lft = el[r];
+                if (v == V - 1 && L.lane == 63) rgt = er[r];
+            }
+            float4 o;
+            o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[k].x, N.row[k].x, xi[k].a, A);
+            o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[k].y, N.row[k].y, xi[k].b, A);
+            o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[k].z, N.row[k].z, xi[k].c, A);
+            o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[k].w, N.row[k].w, xi[k].d, A);
+            const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+            bad |= (int)(m >= A.clampv);
+            if (L.rows_ok) bstore4(ws, L.voff[k], o);
         }
-        float4 o;
-        o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[r].x, N.row[r].x, xi[r].a, A);
-        o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[r].y, N.row[r].y, xi[r].b, A);
-        o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[r].z, N.row[r].z, xi[r].c, A);
-        o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[r].w, N.row[r].w, xi[r].d, A);
-        const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-        bad |= (int)(m >= A.clampv);
-        if (L.rows_ok) bstore4(ws, L.voff[r], o);
     }
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, bool MS, bool NZ>
-__device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R> &L,
-                                           const Slot<R> &P, const Slot<R> &C, Slot<R> &N, int z,
-                                           int zend, size_t plane, uint32_t pbytes, uint32_t qplane,
-                                           int &bad) {
-    load_slot<QX, R>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+template <int QX, int R, int V, bool MS, bool NZ>
+__device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
+                                           const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
+                                           int z, int zend, size_t plane, uint32_t pbytes,
+                                           uint32_t qplane, int &bad) {
+    load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+    plane_compute<QX, R, V, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
 // whole plane of work ahead of its use), then update plane z.
-template <int QX, int R, bool MS, bool NZ>
-__device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX, R> &L,
-                                            const Slot<R> &P, const Slot<R> &C, const Slot<R> &N,
-                                            Slot<R> &F, int z, int zend, size_t plane, uint32_t pbytes,
-                                            uint32_t qplane, int &bad) {
-    if (z + 2 <= zend) load_slot<QX, R>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
-    plane_compute<QX, R, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+template <int QX, int R, int V, bool MS, bool NZ>
+__device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
+                                            const Slot<R, V> &P, const Slot<R, V> &C,
+                                            const Slot<R, V> &N, Slot<R, V> &F, int z, int zend,
+                                            size_t plane, uint32_t pbytes, uint32_t qplane, int &bad) {
+    if (z + 2 <= zend) load_slot<QX, R, V>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
+    plane_compute<QX, R, V, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
-template <int QX, int R, bool MS, bool NZ, int PF>
+template <int QX, int R, int V, bool MS, bool NZ, int PF>
 __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     constexpr int RS = 64 / QX;  // row sets per wave
     const int nb = gridDim.x, b = blockIdx.x;
@@ -241,11 +263,12 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     const size_t plane = (size_t)Lx * (size_t)Ly;
     const uint32_t pbytes = (uint32_t)(plane * sizeof(float));
     const uint32_t qplane = (uint32_t)(plane >> 2);
-    Lane<QX, R> L;
+    Lane<QX, R, V> L;
     L.lane = threadIdx.x & 63;
     const int xq = L.lane & (QX - 1);
     const int rsid = L.lane / QX;
-    const int x = xs * (4 * QX) + 4 * xq;
+    const int xspan = xs * (4 * QX * V);     // first site of this wave's x-span
+    const int x = xspan + 4 * xq;            // segment 0; segment v adds 4*QX*v
     // lanes whose rows fall past Ly (narrow lattices: a wave covers more rows
     // than Ly has) read row 0 and store nothing; shuffles stay inside their
     // x-segment group, which is idle as a whole.
@@ -254,43 +277,50 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     const int y0 = L.rows_ok ? y0r : 0;
     const int ym = y0 == 0 ? Ly - 1 : y0 - 1;
     const int yp = (y0 + R == Ly) ? 0 : y0 + R;
-    const int xl = (x == 0 ? Lx : x) - 1;
-    const int xr = (x + 4 == Lx) ? 0 : x + 4;
+    const int xl = (xspan == 0 ? Lx : xspan) - 1;                                 // MS: left of the span
+    const int xr = (xspan + 4 * QX * V == Lx) ? 0 : xspan + 4 * QX * V;           // MS: right of the span
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        L.voff[r] = (uint32_t)(((y0 + r) * Lx + x) * 4);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int xv = x + 4 * QX * v;
+            L.voff[r * V + v] = (uint32_t)(((y0 + r) * Lx + xv) * 4);
+            L.qoff[r * V + v] = (uint32_t)(((y0 + r) * Lx + xv) >> 2);
+        }
         L.vl[r] = (uint32_t)(((y0 + r) * Lx + xl) * 4);
         L.vr[r] = (uint32_t)(((y0 + r) * Lx + xr) * 4);
-        L.qoff[r] = (uint32_t)(((y0 + r) * Lx + x) >> 2);
     }
-    L.vm = (uint32_t)((ym * Lx + x) * 4);
-    L.vp = (uint32_t)((yp * Lx + x) * 4);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        L.vm[v] = (uint32_t)((ym * Lx + x + 4 * QX * v) * 4);
+        L.vp[v] = (uint32_t)((yp * Lx + x + 4 * QX * v) * 4);
+    }
 
-    Slot<R> S0, S1, S2;
-    load_slot<QX, R>(A, L, S0, zbeg - 1, false, plane, pbytes);
-    load_slot<QX, R>(A, L, S1, zbeg, true, plane, pbytes);
+    Slot<R, V> S0, S1, S2;
+    load_slot<QX, R, V>(A, L, S0, zbeg - 1, false, plane, pbytes);
+    load_slot<QX, R, V>(A, L, S1, zbeg, true, plane, pbytes);
     int bad = 0;
     if constexpr (PF == 1) {
         // three-slot register queue, unrolled so no rotation moves are needed
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
         }
     } else {
         // four-slot queue, prefetch distance 2
-        Slot<R> S3;
-        load_slot<QX, R>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
+        Slot<R, V> S3;
+        load_slot<QX, R, V>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
         for (int z = zbeg; z < zend; z += 4) {
-            plane_step2<QX, R, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
-            plane_step2<QX, R, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, bad);
             if (z + 2 >= zend) break;
-            plane_step2<QX, R, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
             if (z + 3 >= zend) break;
-            plane_step2<QX, R, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, bad);
         }
     }
     if (!L.rows_ok) bad = 0;
@@ -385,20 +415,23 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     else if (Lx < 256 && Lx >= 8 && 64 % (Lx / 4) == 0) qx = Lx / 4;
     else return false;
     const int rs = 64 / qx;
-    // Rows per lane (measured, profiles/r01/sweep*): one row per lane wins when
-    // a wave spans the whole x row (more waves in flight, fewer VGPRs); with
-    // several x segments per row two rows amortise the segment-edge loads.
-    const bool one_seg = Lx <= 256;
-    const int rcand[3] = {one_seg ? 1 : 2, one_seg ? 2 : 4, one_seg ? 4 : 1};
+    // x-span per wave: two 256-site segments per lane when the row is a
+    // multiple of 512 (one wave per 512-site span, no segment-edge loads);
+    // rows per lane (measured, profiles/r01/sweep*): one row per lane wins
+    // for one-segment spans; several spans per row amortise their edge loads
+    // over two rows.
+    const int v = (qx == 64 && Lx % 512 == 0) ? 2 : 1;
+    const bool one_span = Lx == 4 * qx * v;
+    const int rcand[3] = {one_span ? 1 : 2, one_span ? 2 : 4, one_span ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
         if (Ly % (rs * r) == 0) {
-            *g = Phi4Geom{qx, r, rs * r, 1};
+            *g = Phi4Geom{qx, r, rs * r, 1, v};
             return true;
         }
     }
     for (int r : rcand) {  // otherwise a partial last tile (rows past Ly idle)
         if (Ly % r == 0) {
-            *g = Phi4Geom{qx, r, rs * r, 1};
+            *g = Phi4Geom{qx, r, rs * r, 1, v};
             return true;
         }
     }
@@ -406,43 +439,41 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
 }
 
 void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g) {
-    a.nxseg = a.Lx / (4 * g.qx);
+    a.nxseg = a.Lx / (4 * g.qx * g.v);
     a.nyg = (a.Ly + g.wy - 1) / g.wy;
     a.nunits = a.nxseg * a.nyg * a.nzc;
 }
 
-template <int QX, int R, bool MS, bool NZ, int PF>
+template <int QX, int R, int V, bool MS, bool NZ, int PF>
 static hipError_t launch_pf(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
                             hipEvent_t e1) {
     if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ, PF>), grid, dim3(256), 0, s, e0, e1, 0, a);
+        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF>), grid, dim3(256), 0, s, e0, e1, 0, a);
     else
-        hipLaunchKernelGGL((phi4_step_kernel<QX, R, MS, NZ, PF>), grid, dim3(256), 0, s, a);
+        hipLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF>), grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
-template <int QX, int R, bool MS, bool NZ>
-static hipError_t launch_nz(const Phi4StepArgs &a, int pf, dim3 grid, hipStream_t s, hipEvent_t e0,
-                            hipEvent_t e1) {
-    if constexpr (QX == 64)  // the deeper queue is only built for full-row waves
-        if (pf == 2) return launch_pf<QX, R, MS, NZ, 2>(a, grid, s, e0, e1);
-    return launch_pf<QX, R, MS, NZ, 1>(a, grid, s, e0, e1);
+template <int QX, int R, int V, bool MS>
+static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hipStream_t s,
+                           hipEvent_t e0, hipEvent_t e1) {
+    if constexpr (QX == 64 && V == 1) {  // the deeper queue is built for full-row, one-segment waves
+        if (pf == 2)
+            return nz ? launch_pf<QX, R, V, MS, true, 2>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 2>(a, grid, s, e0, e1);
+    }
+    return nz ? launch_pf<QX, R, V, MS, true, 1>(a, grid, s, e0, e1)
+              : launch_pf<QX, R, V, MS, false, 1>(a, grid, s, e0, e1);
 }
 
-template <int QX, int R, bool MS>
-static hipError_t launch_one(const Phi4StepArgs &a, int pf, dim3 grid, hipStream_t s, hipEvent_t e0,
-                             hipEvent_t e1) {
-    return a.sig != 0.0f ? launch_nz<QX, R, MS, true>(a, pf, grid, s, e0, e1)
-                         : launch_nz<QX, R, MS, false>(a, pf, grid, s, e0, e1);
-}
-
-template <int QX, bool MS>
-static hipError_t launch_qx(const Phi4StepArgs &a, int r, int pf, dim3 grid, hipStream_t s,
-                            hipEvent_t e0, hipEvent_t e1) {
-    switch (r) {
-    case 4: return launch_one<QX, 4, MS>(a, pf, grid, s, e0, e1);
-    case 2: return launch_one<QX, 2, MS>(a, pf, grid, s, e0, e1);
-    default: return launch_one<QX, 1, MS>(a, pf, grid, s, e0, e1);
+template <int QX, int V, bool MS>
+static hipError_t launch_r(const Phi4StepArgs &a, const Phi4Geom &g, dim3 grid, hipStream_t s,
+                           hipEvent_t e0, hipEvent_t e1) {
+    const bool nz = a.sig != 0.0f;
+    switch (g.r) {
+    case 4: return launch_v<QX, 4, V, MS>(a, g.pf, nz, grid, s, e0, e1);
+    case 2: return launch_v<QX, 2, V, MS>(a, g.pf, nz, grid, s, e0, e1);
+    default: return launch_v<QX, 1, V, MS>(a, g.pf, nz, grid, s, e0, e1);
     }
 }
 
@@ -450,15 +481,16 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
                             hipEvent_t e1) {
     if (a.nunits <= 0) return hipSuccess;
     const dim3 grid((unsigned)((a.nunits + 3) / 4));
+    const bool ms = a.nxseg > 1;
     switch (g.qx) {
     case 64:
-        return a.nxseg > 1 ? launch_qx<64, true>(a, g.r, g.pf, grid, s, e0, e1)
-                           : launch_qx<64, false>(a, g.r, g.pf, grid, s, e0, e1);
-    case 32: return launch_qx<32, false>(a, g.r, g.pf, grid, s, e0, e1);
-    case 16: return launch_qx<16, false>(a, g.r, g.pf, grid, s, e0, e1);
-    case 8: return launch_qx<8, false>(a, g.r, g.pf, grid, s, e0, e1);
-    case 4: return launch_qx<4, false>(a, g.r, g.pf, grid, s, e0, e1);
-    case 2: return launch_qx<2, false>(a, g.r, g.pf, grid, s, e0, e1);
+        if (g.v == 2) return ms ? launch_r<64, 2, true>(a, g, grid, s, e0, e1) : launch_r<64, 2, false>(a, g, grid, s, e0, e1);
+        return ms ? launch_r<64, 1, true>(a, g, grid, s, e0, e1) : launch_r<64, 1, false>(a, g, grid, s, e0, e1);
+    case 32: return launch_r<32, 1, false>(a, g, grid, s, e0, e1);
+    case 16: return launch_r<16, 1, false>(a, g, grid, s, e0, e1);
+    case 8: return launch_r<8, 1, false>(a, g, grid, s, e0, e1);
+    case 4: return launch_r<4, 1, false>(a, g, grid, s, e0, e1);
+    case 2: return launch_r<2, 1, false>(a, g, grid, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
 }

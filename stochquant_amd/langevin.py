@@ -216,8 +216,8 @@ class Phi4Lattice(_Ctx):
 
     @property
     def tile(self):
-        """(lanes per x segment, rows per lane, z planes per wave) of the step kernel."""
-        out = (ctypes.c_int * 3)()
+        """(lanes per x segment, rows per lane, z planes per wave, float4 segments per lane)."""
+        out = (ctypes.c_int * 4)()
         _lib.call("sq_phi4_tile", self._h, out)
         return tuple(out)
 

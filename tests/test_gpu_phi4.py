@@ -25,7 +25,7 @@ STEP_RTOL = 2.5e-7
 
 SHAPES = [
     (8, 8, 8), (16, 16, 16), (32, 32, 32), (32, 8, 13), (64, 16, 8), (128, 16, 9),
-    (256, 8, 8), (256, 4, 33), (512, 4, 4), (768, 2, 5),
+    (256, 8, 8), (256, 4, 33), (512, 4, 4), (768, 2, 5), (1024, 2, 4), (1536, 2, 3),
 ]
 
 
@@ -246,6 +246,21 @@ def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     monkeypatch.setenv("SQ_PREFETCH", str(pf))
     phi0 = _init(oracle_mod, shape)
     with _lat(shape, C=0.0) as L:
+        L.upload(phi0)
+        L.step(3)
+        got = L.download()
+    assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
+
+
+@pytest.mark.parametrize("shape", [(512, 4, 6), (1024, 2, 5), (512, 8, 9)])
+@pytest.mark.parametrize("vseg", [1, 2])
+def test_segments_per_lane_bitwise(gpu, oracle_mod, monkeypatch, shape, vseg):
+    """V float4 segments per lane (x = 256 v + 4 lane) vs separate waves per
+    256-site segment with edge loads: both bit-identical to the oracle."""
+    monkeypatch.setenv("SQ_VSEG", str(vseg))
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, C=0.0) as L:
+        assert L.tile[3] == vseg
         L.upload(phi0)
         L.step(3)
         got = L.download()
