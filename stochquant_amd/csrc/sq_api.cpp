@@ -448,7 +448,7 @@ int create_phi4(sq_ctx *c) {
     const int nz_max = c->slabs[0].nz;
     // measured optima (profiles/r01/sweep*): zc = 4 for one-segment rows (256^3),
     // zc = 8 when rows span several 256-site segments (512^3)
-    int zc = c->Lx > 4 * c->geom.qx * c->geom.v ? 8 : 4;
+    int zc = c->Lx > 256 ? 8 : 4;
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     c->zc = zc;

@@ -416,13 +416,12 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     else return false;
     const int rs = 64 / qx;
     // x-span per wave: two 256-site segments per lane when the row is a
-    // multiple of 512 (one wave per 512-site span, no segment-edge loads);
-    // rows per lane (measured, profiles/r01/sweep*): one row per lane wins
-    // for one-segment spans; several spans per row amortise their edge loads
-    // over two rows.
+    // multiple of 512 (one wave per 512-site span, no segment-edge loads).
+    // Measured (profiles/r01/sweep*): 256-wide rows (256^3 is MALL-resident)
+    // want R = 1, zc = 4; 512-wide and wider rows (HBM-bound) want R = 2, zc = 8.
     const int v = (qx == 64 && Lx % 512 == 0) ? 2 : 1;
-    const bool one_span = Lx == 4 * qx * v;
-    const int rcand[3] = {one_span ? 1 : 2, one_span ? 2 : 4, one_span ? 4 : 1};
+    const bool narrow = Lx <= 256;
+    const int rcand[3] = {narrow ? 1 : 2, narrow ? 2 : 4, narrow ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
         if (Ly % (rs * r) == 0) {
             *g = Phi4Geom{qx, r, rs * r, 1, v};
