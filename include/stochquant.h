@@ -119,6 +119,17 @@ int sq_phi4_tile(sq_ctx *ctx, int out[4]);
  * phi^2, out[2] = max |phi| (double accumulation on device). */
 int sq_moments(sq_ctx *ctx, double out[3]);
 
+/* The context's parameters (deltatau = the current, possibly adapted, Δτ). */
+int sq_get_params(sq_ctx *ctx, sq_params *out);
+
+/* PHI4 binary checkpoint of this process' slab: <path>
+ * is a NumPy .npy float32 array of shape (nz, Ly, Lx); <path>.json holds the
+ * lattice dims, z0, the Philox step counter, Δτ and the seed.  Replaces the
+ * reference's text end/start file (tauhost.c:91-173,562-581) for 3-D fields.
+ * sq_load_field with restore_counters != 0 also restores step and Δτ. */
+int sq_save_field(sq_ctx *ctx, const char *path);
+int sq_load_field(sq_ctx *ctx, const char *path, int restore_counters);
+
 /* Δτ (dt_mem_obj, tauhost.c:346,526,540). */
 int sq_set_dtau(sq_ctx *ctx, double dtau);
 int sq_get_dtau(sq_ctx *ctx, double *dtau);

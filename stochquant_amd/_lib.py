@@ -90,6 +90,9 @@ SIGNATURES = {
     "sq_slab": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     "sq_moments": (ctypes.c_int, [_P, _D]),
     "sq_phi4_tile": (ctypes.c_int, [_P, _I]),
+    "sq_get_params": (ctypes.c_int, [_P, ctypes.POINTER(SqParams)]),
+    "sq_save_field": (ctypes.c_int, [_P, ctypes.c_char_p]),
+    "sq_load_field": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
     "sq_set_dtau": (ctypes.c_int, [_P, ctypes.c_double]),
     "sq_get_dtau": (ctypes.c_int, [_P, _D]),
     "sq_get_step": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),

@@ -81,6 +81,8 @@ double host_intconst(int pot) {  // tau_kernel.cl:196-200,237-246 (float arithme
 
 }  // namespace
 
+int sq::set_error(int code, const std::string &msg) { return fail(code, msg); }
+
 struct sq_ctx {
     sq_params p{};
     int dev = 0;
@@ -863,6 +865,13 @@ int sq_moments(sq_ctx *c, double out[3]) {
         out[1] += acc[1];
         out[2] = std::max(out[2], (double)fm);
     }
+    return SQ_OK;
+}
+
+int sq_get_params(sq_ctx *c, sq_params *out) {
+    if (!c || !out) return fail(SQ_E_ARG, "null argument");
+    *out = c->p;
+    out->deltatau = c->dtau;
     return SQ_OK;
 }
 

@@ -4,7 +4,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace sq {
+
+// Sets the thread-local message returned by sq_last_error(); returns code.
+int set_error(int code, const std::string &msg);
 
 // ---------------------------------------------------------------- PHI4 ----
 // One slab lives in a padded buffer of (nz + 2*gz) planes of Lx*Ly floats, z

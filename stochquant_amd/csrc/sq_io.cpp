@@ -1,0 +1,151 @@
+// sq_io.cpp -- binary checkpoint of a phi^4 slab (the
+// reference's text start/end file, tauhost.c:91-173,562-581, is impractical at
+// 10^7 sites).  A checkpoint is two files:
+//   <path>        NumPy .npy v1.0, little-endian float32, shape (nz, Ly, Lx)
+//                 (z slowest: exactly the slab's memory order), loadable by np.load;
+//   <path>.json   {"format": "stochquant-phi4-slab", "version": 1, "dims": [Lx,Ly,Lz],
+//                  "z0": ..., "nz": ..., "step": ..., "dtau": ..., "seed": ...}
+// The Philox step counter is saved so a resumed run continues the same noise
+// stream; Δτ is restored (the reference caps it at argv Δτ on resume, :131-136,
+// which callers may apply).
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/stochquant.h"
+#include "sq_internal.h"
+
+namespace {
+
+int io_fail(const std::string &m) { return sq::set_error(SQ_E_ARG, m); }
+
+bool write_npy(const char *path, const float *data, long long nz, long long ny, long long nx) {
+    FILE *fp = fopen(path, "wb");
+    if (!fp) return false;
+    char dict[256];
+    snprintf(dict, sizeof dict, "{'descr': '<f4', 'fortran_order': False, 'shape': (%lld, %lld, %lld), }",
+             nz, ny, nx);
+    std::string hdr(dict);
+    const size_t pre = 10;  // magic(6) + version(2) + header length(2)
+    size_t total = pre + hdr.size() + 1;
+    const size_t pad = (64 - total % 64) % 64;
+    hdr.append(pad, ' ');
+    hdr.push_back('\n');
+    const unsigned short hl = (unsigned short)hdr.size();
+    const unsigned char magic[8] = {0x93, 'N', 'U', 'M', 'P', 'Y', 1, 0};
+    bool ok = fwrite(magic, 1, 8, fp) == 8;
+    const unsigned char hlb[2] = {(unsigned char)(hl & 0xFF), (unsigned char)(hl >> 8)};
+    ok = ok && fwrite(hlb, 1, 2, fp) == 2;
+    ok = ok && fwrite(hdr.data(), 1, hdr.size(), fp) == hdr.size();
+    const size_t n = (size_t)(nz * ny * nx);
+    ok = ok && fwrite(data, sizeof(float), n, fp) == n;
+    return fclose(fp) == 0 && ok;
+}
+
+bool read_npy(const char *path, std::vector<float> &out, long long shape[3]) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) return false;
+    unsigned char head[10];
+    bool ok = fread(head, 1, 10, fp) == 10 && head[0] == 0x93 && memcmp(head + 1, "NUMPY", 5) == 0 &&
+              head[6] == 1;
+    std::string hdr;
+    if (ok) {
+        const size_t hl = head[8] | ((size_t)head[9] << 8);
+        hdr.resize(hl);
+        ok = fread(&hdr[0], 1, hl, fp) == hl;
+    }
+    ok = ok && hdr.find("'<f4'") != std::string::npos && hdr.find("'fortran_order': False") != std::string::npos;
+    const size_t sp = ok ? hdr.find("'shape': (") : std::string::npos;
+    ok = ok && sp != std::string::npos &&
+         sscanf(hdr.c_str() + sp + 10, "%lld, %lld, %lld", &shape[0], &shape[1], &shape[2]) == 3;
+    if (ok) {
+        const size_t n = (size_t)(shape[0] * shape[1] * shape[2]);
+        out.resize(n);
+        ok = fread(out.data(), sizeof(float), n, fp) == n;
+    }
+    fclose(fp);
+    return ok;
+}
+
+long long json_int(const std::string &j, const char *key, bool *found) {
+    const std::string k = std::string("\"") + key + "\":";
+    const size_t p = j.find(k);
+    *found = p != std::string::npos;
+    return *found ? strtoll(j.c_str() + p + k.size(), nullptr, 10) : 0;
+}
+
+double json_dbl(const std::string &j, const char *key, bool *found) {
+    const std::string k = std::string("\"") + key + "\":";
+    const size_t p = j.find(k);
+    *found = p != std::string::npos;
+    return *found ? strtod(j.c_str() + p + k.size(), nullptr) : 0.0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sq_save_field(sq_ctx *ctx, const char *path) {
+    if (!ctx || !path) return io_fail("null argument");
+    int tile[4];
+    if (sq_phi4_tile(ctx, tile) != SQ_OK) return io_fail("sq_save_field: PHI4 contexts only");
+    long long nz = 0, z0 = 0;
+    sq_slab(ctx, &nz, &z0);
+    sq_params P;
+    if (sq_get_params(ctx, &P) != SQ_OK) return io_fail("sq_get_params failed");
+    std::vector<float> f((size_t)(nz * P.dims[1] * P.dims[0]));
+    int rc = sq_download_field(ctx, f.data(), f.size());
+    if (rc) return rc;
+    if (!write_npy(path, f.data(), nz, P.dims[1], P.dims[0])) return io_fail(std::string("cannot write ") + path);
+    unsigned long long step = 0;
+    double dtau = 0;
+    sq_get_step(ctx, &step);
+    sq_get_dtau(ctx, &dtau);
+    const std::string jpath = std::string(path) + ".json";
+    FILE *fp = fopen(jpath.c_str(), "w");
+    if (!fp) return io_fail("cannot write " + jpath);
+    fprintf(fp,
+            "{\"format\": \"stochquant-phi4-slab\", \"version\": 1, \"dims\": [%lld, %lld, %lld], "
+            "\"z0\": %lld, \"nz\": %lld, \"step\": %llu, \"dtau\": %.17g, \"seed\": %llu}\n",
+            P.dims[0], P.dims[1], P.dims[2], z0, nz, step, dtau, P.seed);
+    return fclose(fp) == 0 ? SQ_OK : io_fail("cannot write " + jpath);
+}
+
+int sq_load_field(sq_ctx *ctx, const char *path, int restore_counters) {
+    if (!ctx || !path) return io_fail("null argument");
+    int tile[4];
+    if (sq_phi4_tile(ctx, tile) != SQ_OK) return io_fail("sq_load_field: PHI4 contexts only");
+    long long nz = 0, z0 = 0;
+    sq_slab(ctx, &nz, &z0);
+    sq_params P;
+    if (sq_get_params(ctx, &P) != SQ_OK) return io_fail("sq_get_params failed");
+    std::vector<float> f;
+    long long shape[3];
+    if (!read_npy(path, f, shape)) return io_fail(std::string("cannot read .npy float32 field ") + path);
+    if (shape[0] != nz || shape[1] != P.dims[1] || shape[2] != P.dims[0])
+        return io_fail("checkpoint shape does not match this slab");
+    int rc = sq_upload_field(ctx, f.data(), f.size());
+    if (rc) return rc;
+    if (restore_counters) {
+        const std::string jpath = std::string(path) + ".json";
+        FILE *fp = fopen(jpath.c_str(), "r");
+        if (!fp) return io_fail("cannot read " + jpath);
+        std::string j;
+        char buf[512];
+        size_t n;
+        while ((n = fread(buf, 1, sizeof buf, fp)) > 0) j.append(buf, n);
+        fclose(fp);
+        bool f1, f2, f3;
+        const long long step = json_int(j, "step", &f1);
+        const double dtau = json_dbl(j, "dtau", &f2);
+        const long long jz0 = json_int(j, "z0", &f3);
+        if (!f1 || !f2 || !f3) return io_fail("incomplete checkpoint metadata " + jpath);
+        if (jz0 != z0) return io_fail("checkpoint z0 does not match this slab");
+        sq_set_step(ctx, (unsigned long long)step);
+        sq_set_dtau(ctx, dtau);
+    }
+    return SQ_OK;
+}
+
+}  // extern "C"

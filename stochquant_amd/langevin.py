@@ -221,6 +221,13 @@ class Phi4Lattice(_Ctx):
         _lib.call("sq_phi4_tile", self._h, out)
         return tuple(out)
 
+    def save(self, path):
+        """Binary checkpoint: <path> (.npy float32 (nz, Ly, Lx)) + <path>.json (step, dtau, seed, z0)."""
+        _lib.call("sq_save_field", self._h, os.fsencode(path))
+
+    def load(self, path, restore_counters=True):
+        _lib.call("sq_load_field", self._h, os.fsencode(path), 1 if restore_counters else 0)
+
     def correlator(self, n=None):
         n = self.shape[2] if n is None else int(n)
         out = np.empty(n)

@@ -265,3 +265,32 @@ def test_segments_per_lane_bitwise(gpu, oracle_mod, monkeypatch, shape, vseg):
         L.step(3)
         got = L.download()
     assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
+
+
+def test_checkpoint_roundtrip_resumes_noise_bitwise(gpu, oracle_mod, tmp_path):
+    """Binary checkpoint (sq_save_field / sq_load_field): save after k steps,
+    load into a fresh context, continue m steps == the uninterrupted k+m run,
+    bit for bit (the Philox step counter and Δτ travel in <path>.json)."""
+    import json
+    shape = (64, 16, 12)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, loops=4) as L:
+        L.upload(phi0)
+        assert L.run_frame()
+        L.save(tmp_path / "ck.npy")
+        saved = L.download()
+        L.step(6)
+        full = L.download()
+        d_full = L.dtau
+    assert np.array_equal(np.load(tmp_path / "ck.npy"), saved)
+    meta = json.loads((tmp_path / "ck.npy.json").read_text())
+    assert meta["dims"] == [64, 16, 12] and meta["step"] == 4 and meta["seed"] == 1234
+    with _lat(shape, loops=4, dtau=0.5) as L:
+        L.load(tmp_path / "ck.npy")
+        assert L.step_counter == 4 and L.dtau == d_full
+        L.step(6)
+        assert np.array_equal(L.download(), full)
+    with _lat((64, 16, 13)) as L:
+        from stochquant_amd import StochQuantError
+        with pytest.raises(StochQuantError):
+            L.load(tmp_path / "ck.npy")
