@@ -37,6 +37,11 @@ extern "C" {
 #define SQ_MODEL_QM1D 0  /* the reference's 1-D chain + collective coordinate (tau_kernel.cl:25-175), fp64 */
 #define SQ_MODEL_PHI4 1  /* 3-D phi^4 lattice, fp32 (north-star extension) */
 
+/* QM1D sweep order (sq_qm1d_set_ordering) */
+#define SQ_ORDER_JACOBI 0   /* default: Jacobi sweep, counter-based Philox noise, one launch per frame */
+#define SQ_ORDER_SERIAL 1   /* the reference's serial order: Gauss-Seidel sweep, shared 48-bit LCG
+                               (tau_kernel.cl:25-175,269-284 with items run in id order) */
+
 /* halo transport for slab decomposition (SQ_MODEL_PHI4 only) */
 #define SQ_COMM_NONE 0      /* one slab, periodic z handled in-kernel */
 #define SQ_COMM_LOOPBACK 1  /* nslabs slabs on this device, halos by D2D copies */
@@ -95,6 +100,22 @@ int sq_download(sq_ctx *ctx, double *f, double *x, double *xx0, double *omega, l
  * and the Philox step counter; for tests and checkpoint/resume. */
 int sq_qm1d_get_scan(sq_ctx *ctx, int *lrgEl, double *lrgVl, unsigned long long *tick);
 int sq_qm1d_set_scan(sq_ctx *ctx, int lrgEl, double lrgVl, unsigned long long tick);
+
+/* QM1D sweep order.  SQ_ORDER_SERIAL reproduces the
+ * serial semantics of time_dev: Gauss-Seidel order,
+ * the last step of a frame Jacobi, the racy stability scan as the in-order
+ * scan, the break after the first unstable item, newf / lrgEl / lrgVl / the
+ * seed never rolled back.  2 <= N <= 4096.  Its noise is the reference's
+ * random() (tau_kernel.cl:269-284) on the shared seed rand1 (tauhost.c:185):
+ * sq_qm1d_set_lcg_seed sets it, each frame advances it by the calls it made
+ * (sq_qm1d_noise_consumed).  sq_qm1d_inject_noise replaces the next frame's
+ * draws with a caller-supplied stream in call order (k = round*(N+1) + item,
+ * n >= (N+1)*loops); the seed is then left alone. */
+int sq_qm1d_set_ordering(sq_ctx *ctx, int ordering);
+int sq_qm1d_set_lcg_seed(sq_ctx *ctx, unsigned long long seed);
+int sq_qm1d_get_lcg_seed(sq_ctx *ctx, unsigned long long *seed);
+int sq_qm1d_inject_noise(sq_ctx *ctx, const double *xi, size_t n);
+int sq_qm1d_noise_consumed(sq_ctx *ctx, unsigned long long *n);
 
 /* One frame = `loops` Langevin steps (one clEnqueueNDRangeKernel + clFinish,
  * tauhost.c:481-483) with the stability read-back :504-505, adoption of the
@@ -162,6 +183,10 @@ int sq_selftest_normals(int device, unsigned long long seed, unsigned int stream
 int sq_selftest_dpp(int device, float *out64x2);
 int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
 int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps);
+/* The serial order's draws of one full launch from `seed` on the device:
+ * words t1>>16, t2>>16, the seed after each call, xi ((N+1)*loops each). */
+int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
+                    unsigned int *w2, unsigned long long *seeds, double *xi);
 
 #ifdef __cplusplus
 }

@@ -32,6 +32,18 @@ class Qm1d(ctypes.Structure):
     ]
 
 
+class SerialDev(ctypes.Structure):
+    """orc_serial_dev: the reference's device buffers + kernel scalars (serial order)."""
+    _fields_ = [
+        ("N", ctypes.c_int), ("pot", ctypes.c_int), ("loops", ctypes.c_int),
+        ("a", ctypes.c_double), ("c", ctypes.c_double),
+        ("f", _D), ("x", _D), ("xx0", _D), ("nf", _D), ("nx", _D), ("nxx0", _D),
+        ("omega", ctypes.c_double), ("seed", ctypes.c_uint64), ("stable", ctypes.c_int),
+        ("dtau", ctypes.c_double), ("lrgEl", ctypes.c_int), ("lrgVl", ctypes.c_double),
+        ("runs", ctypes.c_int),
+    ]
+
+
 class Phi4(ctypes.Structure):
     _fields_ = [
         ("Lx", ctypes.c_int), ("Ly", ctypes.c_int), ("Lz", ctypes.c_int),
@@ -62,6 +74,9 @@ def lib():
         L.orc_intconst.restype = ctypes.c_double
         L.orc_intconst.argtypes = [ctypes.c_int]
         L.orc_qm1d_frame.argtypes = [ctypes.POINTER(Qm1d)]
+        L.orc_serial_launch.argtypes = [ctypes.POINTER(SerialDev)]
+        L.orc_ref_noise_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _D, _U32, _U32,
+                                           ctypes.POINTER(ctypes.c_uint64)]
         L.orc_phi4_step.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_uint64, ctypes.c_int]
         L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_uint64]
@@ -103,6 +118,68 @@ def qm1d_frame(N, a, dtau, pot, C, loops, seed, tick, runs, f, x, xx0, omega, lr
     lib().orc_qm1d_frame(ctypes.byref(s))
     return {"f": nf, "x": nx, "xx0": nxx0, "omega": s.nomega, "lrgEl": s.lrgEl, "lrgVl": s.lrgVl,
             "stable": s.stable, "steps_done": s.steps_done}
+
+
+def ref_noise_stream(seed, N, loops):
+    """The reference's random() draws of one full launch in call order
+    (k = round*(N+1) + item): xi, the accepted draws' words t1>>16 and t2>>16,
+    and the shared seed after each call."""
+    n = (N + 1) * loops
+    xi = np.empty(n)
+    w1 = np.empty(n, dtype=np.uint32)
+    w2 = np.empty(n, dtype=np.uint32)
+    seeds = np.empty(n, dtype=np.uint64)
+    lib().orc_ref_noise_stream(seed, N, loops, xi.ctypes.data_as(_D), w1.ctypes.data_as(_U32),
+                               w2.ctypes.data_as(_U32), seeds.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)))
+    return xi, w1, w2, seeds
+
+
+class SerialChain:
+    """The reference's device state under the serial semantics, frame by frame
+    (orc_serial_launch = one clEnqueueNDRangeKernel of time_dev), with the
+    host loop of tauhost.c:504-554: stable -> adopt new*, runs += loops;
+    either way re-upload f, x, xx0, omega.  newf, lrgEl, lrgVl and the seed
+    are never rolled back (tauhost.c)."""
+
+    def __init__(self, N, a, dtau, pot, C, loops, seed, f, x=None, xx0=None, omega=0.0, runs=0, adapt=True):
+        self.N = N
+        self.adapt = adapt
+        self.stab_cnt = 0
+        self.host = {"f": np.array(f, dtype=np.float64), "x": np.zeros(N) if x is None else np.array(x, float),
+                     "xx0": np.zeros(N) if xx0 is None else np.array(xx0, float)}
+        self.buf = {k: np.array(self.host[k]) for k in ("f", "x", "xx0")}
+        self.buf.update({"nf": np.array(self.host["f"]), "nx": np.array(self.host["x"]),
+                         "nxx0": np.array(self.host["xx0"])})
+        self.d = SerialDev(N=N, pot=pot, loops=loops, a=a, c=C, omega=omega, seed=seed, stable=1,
+                           dtau=dtau, lrgEl=0, lrgVl=0.0, runs=runs)
+        for k, v in self.buf.items():
+            setattr(self.d, k, v.ctypes.data_as(_D))
+        self.omega = omega
+        self.runs = runs
+
+    def frame(self):
+        d = self.d
+        lib().orc_serial_launch(ctypes.byref(d))
+        stable = d.stable
+        if stable == 1:
+            for k in ("f", "x", "xx0"):
+                self.host[k][:] = self.buf["n" + k]
+            self.omega = d.omega
+            if self.adapt:                        # tauhost.c:523-528
+                if self.stab_cnt > 10:
+                    self.stab_cnt = 0
+                    d.dtau = d.dtau / 0.950
+                self.stab_cnt += 1
+            self.runs += d.loops
+        elif self.adapt:                          # :537-541
+            d.dtau = d.dtau * 0.950
+            self.stab_cnt = 0
+        d.stable = 1
+        for k in ("f", "x", "xx0"):
+            self.buf[k][:] = self.host[k]
+        d.omega = self.omega
+        d.runs = self.runs
+        return stable
 
 
 def phi4_params(shape, h, m2, lam, seed, clamp=1000.0, C=1.0):

@@ -69,7 +69,9 @@ void orc_normals4(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, 
  * compares `== 1`, tau_kernel.cl:130,282). */
 static int cl_isinf(float v) { return isinf(v) ? 1 : 0; }
 
-double orc_ref_random(uint64_t *seed, int gid)
+/* One call of random(); w1, w2 (if non-NULL) get the 32-bit words t1>>16,
+ * t2>>16 of the accepted (non-retried) draw. */
+static double ref_random_words(uint64_t *seed, int gid, uint32_t *w1, uint32_t *w2)
 {
     const uint64_t mask48 = (((uint64_t)1) << 48) - 1;
     const uint64_t two31 = (uint64_t)2147483648.0f;   /* (ulong)pown((float)2,31) */
@@ -78,9 +80,12 @@ double orc_ref_random(uint64_t *seed, int gid)
     uint64_t t;
     do {
         t = ((*seed + (uint64_t)gid) * 0x5DEECE66DULL + 0xBULL) & mask48;
+        const uint32_t a1 = (uint32_t)(t >> 16);
         double v1 = (double)(t >> 16) / two32;
         t = ((t + (uint64_t)gid) * 0x5DEECE66DULL + 0xBULL) & mask48;
         double v2 = (double)(t >> 16) / two32;
+        if (w1) *w1 = a1;
+        if (w2) *w2 = (uint32_t)(t >> 16);
         float lg = logf((float)v1);
         float cs = cosf((float)(2. * 3.1415 * v2));
         float sq = sqrtf((float)(-2. * (double)lg));
@@ -91,4 +96,21 @@ double orc_ref_random(uint64_t *seed, int gid)
             *seed = t - two31;
     } while (cl_isinf((float)result) == 1);
     return result;
+}
+
+double orc_ref_random(uint64_t *seed, int gid) { return ref_random_words(seed, gid, 0, 0); }
+
+/* The draws of one full launch in call order: rounds 0..loops-1, items
+ * 0..N in id order, k = r*(N+1) + g.  seeds[k] is the
+ * shared seed after call k, so a launch that breaks after call k leaves the
+ * seed at seeds[k]. */
+void orc_ref_noise_stream(uint64_t seed, int N, int loops, double *xi, uint32_t *w1, uint32_t *w2,
+                          uint64_t *seeds)
+{
+    size_t k = 0;
+    for (int r = 0; r < loops; ++r)
+        for (int g = 0; g <= N; ++g, ++k) {
+            xi[k] = ref_random_words(&seed, g, &w1[k], &w2[k]);
+            seeds[k] = seed;
+        }
 }

@@ -44,6 +44,10 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
 void orc_normals4(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4]);
 /* The reference's shared-seed LCG + Box-Muller, tau_kernel.cl:269-284. */
 double orc_ref_random(uint64_t *seed, int gid);
+/* All draws of one full launch in call order (k = round*(N+1) + item), the
+ * accepted draws' 32-bit words t1>>16 / t2>>16, and the seed after each call. */
+void orc_ref_noise_stream(uint64_t seed, int N, int loops, double *xi, uint32_t *w1, uint32_t *w2,
+                          uint64_t *seeds);
 
 /* ---------------- physics helpers (tau_kernel.cl:184-267) ---------------- */
 double orc_xcl(double t, double w, int pot);

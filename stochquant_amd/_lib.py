@@ -17,6 +17,8 @@ SQ_MODEL_PHI4 = 1
 SQ_COMM_NONE = 0
 SQ_COMM_LOOPBACK = 1
 SQ_COMM_RCCL = 2
+SQ_ORDER_JACOBI = 0
+SQ_ORDER_SERIAL = 1
 
 
 class StochQuantUnavailable(RuntimeError):
@@ -93,6 +95,14 @@ SIGNATURES = {
     "sq_get_params": (ctypes.c_int, [_P, ctypes.POINTER(SqParams)]),
     "sq_save_field": (ctypes.c_int, [_P, ctypes.c_char_p]),
     "sq_load_field": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
+    "sq_qm1d_set_ordering": (ctypes.c_int, [_P, ctypes.c_int]),
+    "sq_qm1d_set_lcg_seed": (ctypes.c_int, [_P, ctypes.c_ulonglong]),
+    "sq_qm1d_get_lcg_seed": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "sq_qm1d_inject_noise": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t]),
+    "sq_qm1d_noise_consumed": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
+    "sq_selftest_lcg": (ctypes.c_int, [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
+                                       ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_double)]),
     "sq_set_dtau": (ctypes.c_int, [_P, ctypes.c_double]),
     "sq_get_dtau": (ctypes.c_int, [_P, _D]),
     "sq_get_step": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),

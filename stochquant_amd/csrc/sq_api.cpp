@@ -100,6 +100,16 @@ struct sq_ctx {
     int lrgEl = 0;
     double lrgVl = 0;
     hipStream_t qstream = nullptr;
+    // QM1D serial order (SQ_ORDER_SERIAL): LCG state and per-frame buffers
+    int order = SQ_ORDER_JACOBI;
+    unsigned long long lcg_seed = 0;  // rand1 (tauhost.c:185), advanced by the calls each frame makes
+    bool inject_pending = false;       // g_xi holds a caller-supplied stream for the next frame
+    unsigned long long consumed = 0;   // random() calls of the last serial frame
+    long long g_calls = 0, g_hist = 0; // capacities
+    double *g_xi = nullptr, *g_om = nullptr, *g_hist_buf = nullptr, *g_nfp = nullptr;
+    uint32_t *g_w1 = nullptr, *g_w2 = nullptr;
+    unsigned long long *g_seeds = nullptr;
+    sq::Qm1dGsState *g_st = nullptr;
     // PHI4
     int Lx = 0, Ly = 0;
     long long Lz = 0;
@@ -484,7 +494,107 @@ int create_qm1d(sq_ctx *c) {
     return SQ_OK;
 }
 
+// Capacity of the serial-order buffers for one full launch.
+int gs_reserve(sq_ctx *c) {
+    const long long calls = (long long)(c->N + 1) * c->p.loops;
+    const long long hist = (long long)c->N * c->p.loops;
+    if (calls > c->g_calls) {
+        (void)hipFree(c->g_xi);
+        (void)hipFree(c->g_w1);
+        (void)hipFree(c->g_w2);
+        (void)hipFree(c->g_seeds);
+        c->g_xi = nullptr;
+        c->g_w1 = c->g_w2 = nullptr;
+        c->g_seeds = nullptr;
+        c->g_calls = 0;
+        SQ_HIP(hipMalloc(&c->g_xi, sizeof(double) * calls));
+        SQ_HIP(hipMalloc(&c->g_w1, sizeof(uint32_t) * calls));
+        SQ_HIP(hipMalloc(&c->g_w2, sizeof(uint32_t) * calls));
+        SQ_HIP(hipMalloc(&c->g_seeds, sizeof(unsigned long long) * calls));
+        c->g_calls = calls;
+    }
+    if (hist > c->g_hist) {
+        (void)hipFree(c->g_hist_buf);
+        (void)hipFree(c->g_om);
+        c->g_hist_buf = c->g_om = nullptr;
+        c->g_hist = 0;
+        SQ_HIP(hipMalloc(&c->g_hist_buf, sizeof(double) * hist));
+        SQ_HIP(hipMalloc(&c->g_om, sizeof(double) * (c->p.loops + 1)));
+        c->g_hist = hist;
+    }
+    if (!c->g_st) SQ_HIP(hipMalloc(&c->g_st, sizeof(sq::Qm1dGsState)));
+    return SQ_OK;
+}
+
+// One launch of time_dev in the reference's serial order (sq_qm1d_gs.hip);
+// host bookkeeping as qm1d_frame, plus the shared seed: it advances by the
+// calls the launch made, whether or not the frame was stable (tauhost.c never
+// rolls it back).
+int qm1d_gs_frame(sq_ctx *c, int *stable) {
+    int rc = gs_reserve(c);
+    if (rc) return rc;
+    const long long calls = (long long)(c->N + 1) * c->p.loops;
+    const bool injected = c->inject_pending;
+    c->inject_pending = false;
+    EvPair *e = nullptr;
+    rc = ev_begin(c, c->qstream, &e);
+    if (rc) return rc;
+    if (!injected)
+        SQ_HIP(sq::qm1d_gs_lcg_launch(c->lcg_seed, c->N, calls, c->g_w1, c->g_w2, c->g_seeds, c->g_xi,
+                                      c->qstream));
+    sq::Qm1dGsArgs a{};
+    const int k = c->qcur;
+    a.f0 = c->qf[k];
+    a.x0 = c->qx[k];
+    a.xx00 = c->qxx0[k];
+    a.nf = c->qf[k ^ 1];
+    a.nx = c->qx[k ^ 1];
+    a.nxx0 = c->qxx0[k ^ 1];
+    a.nfp = c->g_nfp;
+    a.xi = c->g_xi;
+    a.om = c->g_om;
+    a.hist = c->g_hist_buf;
+    a.st = c->g_st;
+    a.N = c->N;
+    a.pot = c->p.pot;
+    a.loops = c->p.loops;
+    a.runs = (int)c->runs;
+    a.a = c->p.deltat;
+    const float fa = (float)c->p.deltat;
+    a.a2 = (double)(fa * fa);
+    a.h = c->dtau;
+    a.sig = c->p.C * (double)sqrtf((float)(2. * c->dtau / c->p.deltat));
+    a.sigw = c->p.C * (double)sqrtf((float)(2. * c->dtau));
+    a.kconst = host_intconst(c->p.pot);
+    sq::Qm1dGsState st{};
+    st.omega_in = c->omega;
+    st.lrgEl = c->lrgEl;
+    st.lrgVl = c->lrgVl;
+    SQ_HIP(hipMemcpyAsync(c->g_st, &st, sizeof st, hipMemcpyHostToDevice, c->qstream));
+    SQ_HIP(sq::qm1d_gs_frame_launch(a, c->qstream));
+    if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
+    SQ_HIP(hipMemcpyAsync(&st, c->g_st, sizeof st, hipMemcpyDeviceToHost, c->qstream));
+    SQ_HIP(hipStreamSynchronize(c->qstream));
+    c->consumed = (unsigned long long)st.consumed;
+    if (!injected && st.consumed > 0)
+        SQ_HIP(hipMemcpy(&c->lcg_seed, c->g_seeds + (st.consumed - 1), sizeof(unsigned long long),
+                         hipMemcpyDeviceToHost));
+    c->step += (unsigned long long)c->p.loops;
+    c->lrgEl = st.lrgEl;
+    c->lrgVl = st.lrgVl;
+    c->perf.steps += st.steps_done;
+    c->perf.site_updates += (long long)st.steps_done * c->N;
+    *stable = st.stable;
+    if (st.stable == 1) {  // tauhost.c:506-532
+        c->qcur ^= 1;
+        c->omega = st.omega_out;
+        c->runs += c->p.loops;
+    }
+    return SQ_OK;
+}
+
 int qm1d_frame(sq_ctx *c, int *stable) {
+    if (c->order == SQ_ORDER_SERIAL) return qm1d_gs_frame(c, stable);
     sq::Qm1dArgs a{};
     const int k = c->qcur;
     a.f = c->qf[k];
@@ -674,6 +784,11 @@ int sq_destroy(sq_ctx *c) {
     }
     (void)hipFree(c->qst);
     for (double *q : c->qscr) (void)hipFree(q);
+    for (double *q : {c->g_xi, c->g_om, c->g_hist_buf, c->g_nfp}) (void)hipFree(q);
+    (void)hipFree(c->g_w1);
+    (void)hipFree(c->g_w2);
+    (void)hipFree(c->g_seeds);
+    (void)hipFree(c->g_st);
     (void)hipFree(c->flag);
     (void)hipFree(c->dacc);
     (void)hipFree(c->dmax);
@@ -694,6 +809,8 @@ int sq_upload(sq_ctx *c, const double *f, const double *x, const double *xx0, do
     SQ_HIP(hipMemcpy(c->qf[c->qcur], f, bytes, hipMemcpyHostToDevice));
     SQ_HIP(hipMemcpy(c->qx[c->qcur], x, bytes, hipMemcpyHostToDevice));
     SQ_HIP(hipMemcpy(c->qxx0[c->qcur], xx0, bytes, hipMemcpyHostToDevice));
+    // the reference writes newf = f once, before the first frame (tauhost.c:177-183,319-377)
+    if (c->g_nfp) SQ_HIP(hipMemcpy(c->g_nfp, f, bytes, hipMemcpyHostToDevice));
     c->omega = omega;
     c->runs = runs;
     return SQ_OK;
@@ -727,6 +844,54 @@ int sq_qm1d_set_scan(sq_ctx *c, int lrgEl, double lrgVl, unsigned long long tick
     c->lrgEl = lrgEl;
     c->lrgVl = lrgVl;
     c->step = tick;
+    return SQ_OK;
+}
+
+int sq_qm1d_set_ordering(sq_ctx *c, int ordering) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (is_phi4(c)) return fail(SQ_E_STATE, "QM1D only");
+    if (ordering != SQ_ORDER_JACOBI && ordering != SQ_ORDER_SERIAL) return fail(SQ_E_ARG, "unknown ordering");
+    if (ordering == SQ_ORDER_SERIAL) {
+        if (sq::qm1d_gs_block(c->N) == 0)
+            return fail(SQ_E_ARG, "SQ_ORDER_SERIAL supports 2 <= N <= " + std::to_string(sq::kQm1dGsMaxN));
+        DeviceGuard g(c->dev);
+        if (!c->g_nfp) {
+            SQ_HIP(hipMalloc(&c->g_nfp, sizeof(double) * (size_t)c->N));
+            SQ_HIP(hipMemcpy(c->g_nfp, c->qf[c->qcur], sizeof(double) * (size_t)c->N, hipMemcpyDeviceToDevice));
+        }
+    }
+    c->order = ordering;
+    return SQ_OK;
+}
+
+int sq_qm1d_set_lcg_seed(sq_ctx *c, unsigned long long seed) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    c->lcg_seed = seed;
+    return SQ_OK;
+}
+
+int sq_qm1d_get_lcg_seed(sq_ctx *c, unsigned long long *seed) {
+    if (!c || !seed) return fail(SQ_E_ARG, "null argument");
+    *seed = c->lcg_seed;
+    return SQ_OK;
+}
+
+int sq_qm1d_inject_noise(sq_ctx *c, const double *xi, size_t n) {
+    if (!c || !xi) return fail(SQ_E_ARG, "null argument");
+    if (is_phi4(c) || c->order != SQ_ORDER_SERIAL) return fail(SQ_E_STATE, "needs a QM1D context in SQ_ORDER_SERIAL");
+    const size_t need = (size_t)(c->N + 1) * (size_t)c->p.loops;
+    if (n < need) return fail(SQ_E_ARG, "need (N+1)*loops draws, got " + std::to_string(n));
+    DeviceGuard g(c->dev);
+    int rc = gs_reserve(c);
+    if (rc) return rc;
+    SQ_HIP(hipMemcpy(c->g_xi, xi, sizeof(double) * need, hipMemcpyHostToDevice));
+    c->inject_pending = true;
+    return SQ_OK;
+}
+
+int sq_qm1d_noise_consumed(sq_ctx *c, unsigned long long *n) {
+    if (!c || !n) return fail(SQ_E_ARG, "null argument");
+    *n = c->consumed;
     return SQ_OK;
 }
 
@@ -1014,6 +1179,28 @@ int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int
     hipError_t e = hipMemcpy(d, h, sizeof h, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = sq::selftest_philox_launch(d, d + 6, nullptr);
     if (e == hipSuccess) e = hipMemcpy(out, d + 6, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
+int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
+                    unsigned int *w2, unsigned long long *seeds, double *xi) {
+    if (!w1 || !w2 || !seeds || !xi || N < 1 || loops < 1) return fail(SQ_E_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    const long long n = (long long)(N + 1) * loops;
+    char *d = nullptr;
+    SQ_HIP(hipMalloc(&d, (size_t)n * 24));
+    uint32_t *dw1 = (uint32_t *)d, *dw2 = dw1 + n;
+    unsigned long long *ds = (unsigned long long *)(dw2 + n);
+    double *dx = (double *)(ds + n);
+    hipError_t e = sq::qm1d_gs_lcg_launch(seed, N, n, dw1, dw2, ds, dx, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(w1, dw1, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(w2, dw2, n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(seeds, ds, n * 8, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(xi, dx, n * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d);
     if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
     return SQ_OK;

@@ -84,6 +84,31 @@ int qm1d_sites_per_thread(int N);  // 0 if N unsupported; > 8 = global-memory va
 constexpr int kQm1dMaxN = 1024 * 64;
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
 
+// QM1D in the reference's serial order (sq_qm1d_gs.hip)
+struct Qm1dGsState {
+    double omega_in, omega_out, lrgVl;
+    int lrgEl, stable, steps_done, pad;
+    long long consumed;  // random() calls the launch made (the shared seed advances by these)
+};
+
+struct Qm1dGsArgs {
+    const double *f0, *x0, *xx00;  // frame-start state (N)
+    double *nf, *nx, *nxx0;        // state after a stable frame (N)
+    double *nfp;                   // the persistent newf buffer (never rolled back, tauhost.c)
+    const double *xi;              // (N+1)*loops draws in call order
+    double *om;                    // omega at the start of each step (loops+1)
+    double *hist;                  // field after each step (loops*N)
+    Qm1dGsState *st;
+    int N, pot, loops, runs;
+    double a, a2, h, sig, sigw, kconst;
+};
+
+constexpr int kQm1dGsMaxN = 4096;
+int qm1d_gs_block(int N);  // sites per lane of the sweep pipeline, 0 if N unsupported
+hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
+                              uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s);
+hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s);
+
 // -------------------------------------------------------------- selftest --
 hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long quad0,
                                    uint32_t stream, unsigned long long step, uint32_t k0,

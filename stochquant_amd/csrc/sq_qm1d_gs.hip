@@ -1,0 +1,393 @@
+// sq_qm1d_gs.hip -- QM1D in the reference's own serial order (SURVEY.md §8f
+// row 4): Gauss-Seidel sweep, one shared 48-bit LCG, the stability scan and
+// running means exactly as time_dev runs when its work-items execute in id
+// order between barriers (oracle/orc_qm1d.c serial).
+//
+// Four launches per frame, all on one stream:
+//   gs_lcg_kernel    one wave, scalar: the LCG of tau_kernel.cl:269-284 for
+//                    every call of a full launch (rounds 0..loops-1, items
+//                    0..N), incl. the isinf retry; stores the accepted draw's
+//                    words t1>>16, t2>>16 and the seed after each call.  The
+//                    recurrence is inherently serial (the seed update is
+//                    non-linear), so this is the frame's floor.
+//   gs_xi_kernel     grid-wide: xi = cos(2*3.1415*v2) * sqrt(-2 log v1) with
+//                    the reference's float casts (correctly rounded float
+//                    log/cos via fp64; glibc's logf/cosf round differently in
+//                    ~1% of arguments, so xi is within 1 ulp of the oracle's,
+//                    and bit-exact when the stream is injected).
+//   gs_sweep_kernel  one wave: the GS field sweep as a skewed pipeline.  Lane l
+//                    owns sites [lB, lB+B) and runs step j in phase p = l + j:
+//                    the left neighbour's step-j value comes from lane l-1's
+//                    previous phase, the right neighbour's step-(j-1) value
+//                    from lane l+1's first site of the same phase.  Every
+//                    (step, site) is computed exactly as the serial order
+//                    computes it, with the reference's expression order.  The
+//                    field of every step goes to hist (loops x N).
+//   gs_scan_kernel   one wave: walks the steps in order and evaluates the
+//                    stability scan (tau_kernel.cl:135-143) as prefix maxima
+//                    (derivation in DESIGN.md §QM1D serial mode), finds the
+//                    first unstable item (the serial break: items after it
+//                    never run that round) and the running means :144-145.
+#include <algorithm>
+
+#include "sq_internal.h"
+
+namespace sq {
+
+namespace {
+
+constexpr double kEta = .8;  // tau_kernel.cl:19-22
+constexpr double kV0 = 2.;
+constexpr double kM = 1.;
+constexpr double kMax = 1000.;
+
+__device__ __forceinline__ double xcl(double t, double w, int pot) {  // clas(), :184-189,215-226
+    if (pot == 3) {
+        const double s = 2.0;  // (double)sqrtf((float)(2.*V0/m)) == 2 exactly
+        return kEta * (double)tanhf((float)(s * (t - w) / kEta));
+    }
+    return 0.;
+}
+__device__ __forceinline__ double ddpot(double x, int pot) {  // ddPot(), :190-195,227-236
+    if (pot == 3) return (12. * kV0 * x * x / (kEta * kEta) - 4. * kV0) / (kEta * kEta);
+    return 2.;
+}
+__device__ __forceinline__ double absol(double v) { return v <= 0 ? -v : v; }
+__device__ __forceinline__ double guard(double v) {  // :119-133
+    if (v > kMax) v = kMax;
+    if (v < -kMax) v = -kMax;
+    if (__builtin_isnan(v)) v = kMax;
+    return v;
+}
+
+// ---------------------------------------------------------------- LCG ----
+__global__ __launch_bounds__(64) void gs_lcg_kernel(unsigned long long seed, int N, long long ncalls,
+                                                     uint32_t *w1, uint32_t *w2,
+                                                     unsigned long long *seeds) {
+    const uint64_t mask48 = (1ull << 48) - 1;
+    const uint64_t two31 = 2147483648ull;
+    const int lane = threadIdx.x;
+    uint64_t s = seed;
+    uint32_t a1 = 0, a2 = 0;
+    uint64_t sv = 0;
+    uint64_t g = 0;
+    for (long long k = 0; k < ncalls; ++k) {
+        uint64_t t1, t2;
+        do {  // the isinf retry of :282 fires exactly when t1 >> 16 == 0 (log(0) = -inf)
+            t1 = ((s + g) * 0x5DEECE66DULL + 0xBULL) & mask48;
+            t2 = ((t1 + g) * 0x5DEECE66DULL + 0xBULL) & mask48;
+            s = (s < two31 && t2 < two31) ? s + t2 : t2 - two31;
+        } while ((t1 >> 16) == 0);
+        const int l = (int)(k & 63);
+        if (lane == l) {
+            a1 = (uint32_t)(t1 >> 16);
+            a2 = (uint32_t)(t2 >> 16);
+            sv = s;
+        }
+        if (l == 63 || k == ncalls - 1) {
+            const long long base = k - l;
+            if (lane <= l) {
+                w1[base + lane] = a1;
+                w2[base + lane] = a2;
+                seeds[base + lane] = sv;
+            }
+        }
+        g = (g == (uint64_t)N) ? 0 : g + 1;
+    }
+}
+
+__global__ __launch_bounds__(256) void gs_xi_kernel(const uint32_t *w1, const uint32_t *w2, double *xi,
+                                                     long long n) {
+    const double two32 = 4294967296.0;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (long long)gridDim.x * blockDim.x) {
+        const double v1 = (double)w1[k] / two32;
+        const double v2 = (double)w2[k] / two32;
+        const float lg = (float)log((double)(float)v1);
+        const float cs = (float)cos((double)(float)(2. * 3.1415 * v2));
+        const float sq = sqrtf((float)(-2. * (double)lg));
+        xi[k] = (double)cs * (double)sq;
+    }
+}
+
+// -------------------------------------------------------------- sweep ----
+// Lane l's step j happens in phase l + j.  CH sites per chunk; the chunk's
+// noise is loaded one chunk ahead (the next phase's first chunk while the
+// last chunk of this phase computes).
+template <int CH>
+__global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B) {
+    extern __shared__ double s_f[];  // the field, updated in place (the serial order's f)
+    const int N = A.N, loops = A.loops, pot = A.pot;
+    const int lane = threadIdx.x;
+    const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
+    const int nl = (N + B - 1) / B;
+    const int i0 = lane * B, i1 = min(N, i0 + B);
+    const bool owner = lane < nl;
+
+    for (int i = lane; i < N; i += 64) s_f[i] = A.f0[i];
+    {  // omega of every step: item N's update, :103-110,155-167.  64 draws
+       // per batch land in lanes; the (wave-uniform) recurrence reads them
+       // with readlane, and lane q keeps omega of step jb + q.
+        double w = A.st->omega_in;
+        const double top = (double)(N - 1) * a;
+        for (int jb = 0; jb < loops; jb += 64) {
+            const int nb = min(64, loops - jb);
+            const double dwl = lane < nb ? A.sigw * A.xi[(size_t)(jb + lane) * (N + 1) + N] : 0.;
+            double mine = 0.;
+            for (int q = 0; q < nb; ++q) {
+                if (lane == q) mine = w;
+                const double nw = w + A.kconst * __shfl(dwl, q, 64);
+                if (nw > top) w = 2 * (double)(N - 1) * a - nw;
+                else if (nw < 0) w = -nw;
+                else w = nw;
+            }
+            if (lane < nb) A.om[jb + lane] = mine;
+        }
+        if (lane == 0) A.om[loops] = w;
+    }
+    __syncthreads();
+
+    double lastnew = 0., lastold = 0.;  // my block's last site after / before my current step
+    const int nchunk = (B + CH - 1) / CH;
+    double cur[CH], nxt[CH];
+    auto load_chunk = [&](double (&dst)[CH], int j, int c) {
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const int i = i0 + c * CH + q;
+            dst[q] = (owner && j >= 0 && j < loops && i < i1) ? A.xi[(size_t)j * (N + 1) + i] : 0.;
+        }
+    };
+    load_chunk(cur, -lane, 0);
+    const int nphase = nl - 1 + loops;
+    for (int p = 0; p < nphase; ++p) {
+        const int j = p - lane;
+        const bool act = owner && j >= 0 && j < loops;
+        const bool last = j == loops - 1;
+        const double w = act ? A.om[j] : 0.;
+        const double lnew = __shfl_up(lastnew, 1, 64);
+        const double lold = __shfl_up(lastold, 1, 64);
+        double prev_new = lnew, prev_old = lold, firstval = 0., rfirst = 0.;
+        for (int c = 0; c < nchunk; ++c) {
+            if (c + 1 < nchunk) load_chunk(nxt, j, c + 1);
+            else load_chunk(nxt, j + 1, 0);
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const int b = c * CH + q;
+                const int i = i0 + b;
+                const bool valid = act && i < i1;
+                if (b == B - 1) rfirst = __shfl_down(firstval, 1, 64);  // lane l+1's first site, its step j-1
+                if (b < B) {
+                    const double fi = i < N ? s_f[i] : 0.;
+                    double v = fi;
+                    if (valid) {
+                        const double L = last ? prev_old : prev_new;
+                        double s;
+                        if (i == 0) {
+                            const double R = N > 1 ? s_f[1] : 0.;  // N >= 2; i + 1 < i1 since B >= 2
+                            s = R + (-kEta) - xcl(-1. * a, w, pot) - 2 * fi;
+                        } else if (i == N - 1) {
+                            s = L + kEta - xcl((double)N * a, w, pot) - 2 * fi;
+                        } else {
+                            const double R = b == B - 1 ? rfirst : s_f[i + 1];
+                            s = R + L - 2 * fi;
+                        }
+                        v = fi + kM * h * s / a2 - ddpot(xcl((double)i * a, w, pot), pot) * fi * h + sig * cur[q];
+                        v = guard(v);
+                        A.hist[(size_t)j * N + i] = v;
+                        if (!last) s_f[i] = v;
+                    }
+                    prev_old = fi;
+                    prev_new = v;
+                    if (b == 0) firstval = v;  // = s_f[i0] after this phase's update (old value if idle)
+                    if (b == B - 1 || i == i1 - 1) {
+                        if (i == i1 - 1) {
+                            lastnew = v;
+                            lastold = fi;
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
+        }
+    }
+}
+
+// --------------------------------------------------------------- scan ----
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_excl_max(double v, int lane) {  // max over lanes < lane
+    double incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl = fmax(incl, u);
+    }
+    const double ex = __shfl_up(incl, 1, 64);
+    return lane == 0 ? -__builtin_inf() : ex;
+}
+
+// LDS: f (previous step's field, the serial order's "old f"), nfc (this step),
+// x, xx0 -- 4N doubles.
+__global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
+    extern __shared__ double lds[];
+    const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
+    double *s_f = lds, *s_n = lds + N, *s_x = lds + 2 * N, *s_xx0 = lds + 3 * N;
+    const int lane = threadIdx.x;
+    const int B = (N + 63) / 64;
+    const int i0 = lane * B, i1 = min(N, i0 + B);
+    const double a = A.a, sig = A.sig;
+    const double NEG = -__builtin_inf();
+    for (int i = lane; i < N; i += 64) {
+        s_f[i] = A.f0[i];
+        s_x[i] = A.x0[i];
+        s_xx0[i] = A.xx00[i];
+    }
+    __syncthreads();
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int brk_step = -1, brk_item = -1;
+    for (int j = 0; j < loops; ++j) {
+        const double w = A.om[j];
+        const double *row = A.hist + (size_t)j * N;
+        const double *xr = A.xi + (size_t)j * (N + 1);
+        // nf[E] as the serial order sees it before item E runs this step:
+        // the previous step's value (the persistent newf buffer at j = 0)
+        const double nfE = j == 0 ? A.nfp[E] : s_f[E];
+        const double T0 = nfE + xcl((double)E * a, w, pot);
+        double m1 = NEG;
+        for (int i = i0; i < i1; ++i) {
+            const double v = row[i];
+            s_n[i] = v;
+            if (i < E) m1 = fmax(m1, v + xcl((double)i * a, w, pot));
+        }
+        __syncthreads();
+        const bool caseB = wave_max(m1) > T0;  // a leader before E: no reset at item E
+        // lane totals of Y (X, masked below E in case A) and |X|
+        double ty = NEG, ta = NEG;
+        for (int i = i0; i < i1; ++i) {
+            const double X = s_n[i] + xcl((double)i * a, w, pot);
+            if (caseB || i >= E) ty = fmax(ty, X);
+            ta = fmax(ta, absol(X));
+        }
+        double py = wave_excl_max(ty, lane), pa = wave_excl_max(ta, lane);
+        const double base = caseB ? T0 : NEG;
+        int first_bad = 0x7fffffff, last_lead = -1;
+        double Vbad = 0.;
+        for (int i = i0; i < i1; ++i) {
+            const double X = s_n[i] + xcl((double)i * a, w, pot);
+            const double th = fmax(base, py);
+            const bool lead = (caseB || i > E) && X > th;
+            const double Vi = fmax(V, pa);  // V seen by item i (max over k < i)
+            if (lead) {
+                last_lead = i;
+                const double d = absol(s_n[i] - s_f[i] - sig * xr[i]);
+                if (d > Vi && i < first_bad) {
+                    first_bad = i;
+                    Vbad = fmax(Vi, absol(X));
+                }
+            }
+            if (caseB || i >= E) py = fmax(py, X);
+            pa = fmax(pa, absol(X));
+        }
+        const int kb = wave_min_i(first_bad);
+        if (kb != 0x7fffffff) {  // items after kb never run this round
+            E = kb;
+            V = __shfl(Vbad, kb / B, 64);
+            brk_step = j;
+            brk_item = kb;
+            break;
+        }
+        const int ll = wave_max_i(last_lead);
+        if (ll >= 0) E = ll;
+        V = fmax(V, wave_max(ta));
+        // running means, :144-145 (f[i] old; f[mid] already updated for i > mid
+        // except in the last step, which commits nothing)
+        const double den = (double)(A.runs + j + 1);
+        const double xm = xcl((double)mid * a, w, pot);
+        const double fm_old = s_f[mid], fm_new = s_n[mid];
+        for (int i = i0; i < i1; ++i) {
+            const double g = s_f[i] + xcl((double)i * a, w, pot);
+            const double fm = (i > mid && j < loops - 1) ? fm_new : fm_old;
+            s_xx0[i] = s_xx0[i] + (g * (fm + xm) - s_xx0[i]) / den;
+            s_x[i] = s_x[i] + (g - s_x[i]) / den;
+        }
+        __syncthreads();
+        for (int i = i0; i < i1; ++i) s_f[i] = s_n[i];
+        __syncthreads();
+    }
+    // persistent newf (never rolled back by the host): the last value each item wrote
+    if (brk_step < 0) {
+        for (int i = i0; i < i1; ++i) {
+            A.nf[i] = s_f[i];
+            A.nfp[i] = s_f[i];
+            A.nx[i] = s_x[i];
+            A.nxx0[i] = s_xx0[i];
+        }
+    } else {
+        for (int i = i0; i < i1; ++i)
+            if (i <= brk_item) A.nfp[i] = s_n[i];
+            else if (brk_step > 0) A.nfp[i] = s_f[i];
+    }
+    if (lane == 0) {
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = brk_step < 0 ? 1 : 0;
+        A.st->steps_done = brk_step < 0 ? loops : brk_step + 1;
+        A.st->omega_out = A.om[loops];
+        A.st->consumed = brk_step < 0 ? (long long)loops * (N + 1)
+                                      : (long long)brk_step * (N + 1) + brk_item + 1;
+    }
+}
+
+}  // namespace
+
+int qm1d_gs_block(int N) {
+    if (N < 2 || N > kQm1dGsMaxN) return 0;
+    return N <= 128 ? 2 : (N + 63) / 64;
+}
+
+hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
+                              uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s) {
+    hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(64), 0, s, seed, N, ncalls, w1, w2, seeds);
+    const int blocks = (int)std::min<long long>(2048, (ncalls + 255) / 256);
+    hipLaunchKernelGGL(gs_xi_kernel, dim3(blocks), dim3(256), 0, s, w1, w2, xi, ncalls);
+    return hipGetLastError();
+}
+
+hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
+    const int B = qm1d_gs_block(a.N);
+    if (B == 0) return hipErrorInvalidValue;
+    const size_t lds1 = sizeof(double) * (size_t)a.N, lds4 = 4 * lds1;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e;
+        if ((e = hipFuncSetAttribute((const void *)gs_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(4 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+            return e;
+        for (const void *k : {(const void *)gs_sweep_kernel<2>, (const void *)gs_sweep_kernel<8>})
+            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+                return e;
+        attr = true;
+    }
+    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(64), lds1, s, a, B);
+    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(64), lds1, s, a, B);
+    hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds4, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sq

@@ -14,6 +14,9 @@
 // the OpenCL platform index 2); no tau_kernel.cl is read from the cwd; the
 // kernel is Jacobi-ordered with Philox noise (seeded from the same rand()
 // draw the reference used for its LCG seed, :185; SQ_SEED overrides).
+// SQ_ORDER=serial selects the reference's own serial order instead
+// (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
+// SQ_ORDER_SERIAL in stochquant.h), N <= 4096.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -145,6 +148,16 @@ int main(int argc, char **argv) {
     p.adapt_dtau = 1;
     sq_ctx *ctx = nullptr;
     if (sq_create(&p, &ctx) != SQ_OK) return die("sq_create", nullptr);
+    if (const char *o = getenv("SQ_ORDER")) {
+        if (strcmp(o, "serial") == 0) {
+            if (sq_qm1d_set_ordering(ctx, SQ_ORDER_SERIAL) != SQ_OK) return die("sq_qm1d_set_ordering", ctx);
+            if (sq_qm1d_set_lcg_seed(ctx, seed) != SQ_OK) return die("sq_qm1d_set_lcg_seed", ctx);
+        } else if (strcmp(o, "jacobi") != 0) {
+            fprintf(stderr, "tauhost: SQ_ORDER must be jacobi or serial\n");
+            sq_destroy(ctx);
+            return 1;
+        }
+    }
     if (sq_upload(ctx, f.data(), x.data(), xx0.data(), omega, recSimlgth) != SQ_OK)
         return die("sq_upload", ctx);
 

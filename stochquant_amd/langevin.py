@@ -19,7 +19,8 @@ import subprocess
 import numpy as np
 
 from . import _lib
-from ._lib import SQ_COMM_LOOPBACK, SQ_COMM_NONE, SQ_COMM_RCCL, SQ_MODEL_PHI4, SQ_MODEL_QM1D
+from ._lib import (SQ_COMM_LOOPBACK, SQ_COMM_NONE, SQ_COMM_RCCL, SQ_MODEL_PHI4, SQ_MODEL_QM1D, SQ_ORDER_JACOBI,
+                   SQ_ORDER_SERIAL)
 
 _DP = ctypes.POINTER(ctypes.c_double)
 _FP = ctypes.POINTER(ctypes.c_float)
@@ -104,7 +105,7 @@ class Qm1dChain(_Ctx):
     `loops` steps per frame (tauhost.c argv[1..10] meaning)."""
 
     def __init__(self, N, deltat, deltatau, pot=3, C=1.0, loops=1000, seed=0x5EED, device=0,
-                 adapt_dtau=True):
+                 adapt_dtau=True, ordering="jacobi", lcg_seed=None):
         p = _lib.default_params()
         p.model = SQ_MODEL_QM1D
         p.dims[0] = int(N)
@@ -118,6 +119,36 @@ class Qm1dChain(_Ctx):
         p.adapt_dtau = 1 if adapt_dtau else 0
         super().__init__(p)
         self.N = int(N)
+        if ordering != "jacobi":
+            self.set_ordering(ordering)
+        if lcg_seed is not None:
+            self.lcg_seed = lcg_seed
+
+    def set_ordering(self, ordering):
+        """"jacobi" (Philox noise, the fast path) or "serial" (the reference's
+        Gauss-Seidel order with its shared-seed LCG, SQ_ORDER_SERIAL)."""
+        _lib.call("sq_qm1d_set_ordering", self._h, {"jacobi": SQ_ORDER_JACOBI, "serial": SQ_ORDER_SERIAL}[ordering])
+
+    @property
+    def lcg_seed(self):
+        v = ctypes.c_ulonglong()
+        _lib.call("sq_qm1d_get_lcg_seed", self._h, ctypes.byref(v))
+        return v.value
+
+    @lcg_seed.setter
+    def lcg_seed(self, v):
+        _lib.call("sq_qm1d_set_lcg_seed", self._h, int(v))
+
+    def inject_noise(self, xi):
+        """Draws for the next serial frame, in call order (round*(N+1) + item)."""
+        xi = np.ascontiguousarray(xi, dtype=np.float64)
+        _lib.call("sq_qm1d_inject_noise", self._h, _dptr(xi), xi.size)
+
+    @property
+    def noise_consumed(self):
+        v = ctypes.c_ulonglong()
+        _lib.call("sq_qm1d_noise_consumed", self._h, ctypes.byref(v))
+        return v.value
 
     def upload(self, f, x=None, xx0=None, omega=0.0, runs=0):
         f = np.ascontiguousarray(f, dtype=np.float64)

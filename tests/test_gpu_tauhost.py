@@ -101,3 +101,53 @@ def test_config_c1_chain_through_tauhost(gpu, tmp_path):
     err = 2 * np.std(bulk ** 2) / np.sqrt(bulk.size) * 3   # ~3 sites correlation length
     assert abs(m2 - g["value"]) < 4 * err
     assert lines[-2].strip() == "1000|N"
+
+
+def _run_env(tmp_path, argv, **env):
+    import os
+    from stochquant_amd import TAUHOST_PATH, run_tauhost
+    a = ["end" if v == "END" else ("start" if v == "START" else v) for v in argv]
+    e = dict(os.environ)
+    e.update(env)
+    r = run_tauhost([TAUHOST_PATH] + list(a), cwd=str(tmp_path), timeout=300, env=e)
+    assert r.returncode == 0, r.stderr.decode()
+    return r.stdout.decode(), (tmp_path / "end").read_text()
+
+
+def _hexrows(text, n):
+    return np.array([[float.fromhex(t.strip()) for t in ln.split("|")] for ln in text.split("\n")[:n]])
+
+
+def test_serial_order_reproduces_appendix_c(gpu, oracle_mod, tmp_path):
+    """SQ_ORDER=serial: the reference's serial order with its LCG seeded from
+    the same rand() draw.  The recorded end file and the
+    serial oracle's whole end file agree to the 1-ulp xi budget (float log/cos
+    rounding, tests/test_gpu_qm1d_serial.py); stdout, omega, N, deltaTau exact."""
+    g = golden("reference_outputs.json")["appendix_c_end_file"]
+    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="serial")
+    assert out.split("\n")[0] == g["stdout_first_line"]
+    el = end.split("\n")
+    assert el[4:7] == g["trailer"]
+    got = _hexrows(end, 4)
+    first = np.array([float.fromhex(t.strip()) for t in g["first_line"].split("|")])
+    assert np.allclose(got[0], first, rtol=1e-6, atol=1e-12)
+    ref_dir = tmp_path / "orc"
+    ref_dir.mkdir()
+    a = ["end" if v == "END" else v for v in g["argv"]]
+    r = oracle_mod.tauhost(a, cwd=str(ref_dir))
+    assert r.returncode == 0
+    ref = _hexrows((ref_dir / "end").read_text(), 4)
+    assert np.allclose(got, ref, rtol=1e-6, atol=1e-12)
+    print("bit-exact sites:", int(np.sum(got == ref)), "of", got.size)
+
+
+def test_serial_order_all_unstable_preset(gpu, tmp_path):
+    """The double-well all-unstable preset in serial order: same printed Δτ
+    sequence and end Δτ / N as the reference's recorded run."""
+    g = golden("reference_outputs.json")["double_well_all_unstable"]
+    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="serial")
+    dt = [ln.split("|")[-2].strip() for ln in out.strip().split("\n")]
+    assert dt == g["printed_dtau"]
+    tail = end.strip().split("\n")[-3:]
+    assert float(tail[2].split("|")[0]) == pytest.approx(g["end_dtau"], rel=1e-6)
+    assert int(tail[1].split("|")[0]) == g["end_N"]
