@@ -27,7 +27,9 @@
 //                    stability scan (tau_kernel.cl:135-143) as prefix maxima
 //                    (derivation in DESIGN.md §QM1D serial mode), finds the
 //                    first unstable item (the serial break: items after it
-//                    never run that round) and the running means :144-145.
+//                    never run that round -- except in round 0, where the
+//                    stable test has not started, :168-171) and the running
+//                    means :144-145.
 #include <algorithm>
 
 #include "sq_internal.h"
@@ -304,7 +306,7 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
             pa = fmax(pa, absol(X));
         }
         const int kb = wave_min_i(first_bad);
-        if (kb != 0x7fffffff) {  // items after kb never run this round
+        if (kb != 0x7fffffff && j > 0) {  // items after kb see stable != 1 and never run this round
             E = kb;
             V = __shfl(Vbad, kb / B, 64);
             brk_step = j;
@@ -314,6 +316,11 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
         const int ll = wave_max_i(last_lead);
         if (ll >= 0) E = ll;
         V = fmax(V, wave_max(ta));
+        if (kb != 0x7fffffff) {  // round 0: the stable test only starts at round 1 (:168-171), all items ran
+            brk_step = 0;
+            brk_item = N;
+            break;
+        }
         // running means, :144-145 (f[i] old; f[mid] already updated for i > mid
         // except in the last step, which commits nothing)
         const double den = (double)(A.runs + j + 1);
@@ -340,7 +347,7 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
     } else {
         for (int i = i0; i < i1; ++i)
             if (i <= brk_item) A.nfp[i] = s_n[i];
-            else if (brk_step > 0) A.nfp[i] = s_f[i];
+            else if (brk_step > 0) A.nfp[i] = s_f[i];  // still the previous round's value
     }
     if (lane == 0) {
         A.st->lrgEl = E;

@@ -95,7 +95,7 @@ def test_injected_noise_unstable_frames_bitwise(gpu, oracle_mod):
     dtau shrinks, the seed advances by the calls made before the break."""
     N, a = 40, 0.1
     f0 = np.random.default_rng(3).standard_normal(N)
-    res = _run_pair(oracle_mod, N, a, 5 * a * a, 0, 1.0, 25, 42, 30, f0, check=_exact)
+    res = _run_pair(oracle_mod, N, a, 5 * a * a, 0, 1.0, 25, 42, 70, f0, check=_exact)
     assert any(r["stable"][0] == 0 for r in res) and any(r["stable"][0] == 1 for r in res)
 
 
@@ -116,8 +116,8 @@ def test_lcg_mode_tracks_reference(gpu, oracle_mod):
         for k in ("stable", "lrgEl", "runs", "seed", "dtau"):
             assert res[k][0] == res[k][1], (res["frame"], k, res[k])
         for k in ("f", "x", "xx0"):
-            assert np.allclose(res[k][0], res[k][1], rtol=0, atol=1e-9), (k, np.max(np.abs(res[k][0] - res[k][1])))
-        assert abs(res["omega"][0] - res["omega"][1]) < 1e-9
+            assert np.allclose(res[k][0], res[k][1], rtol=0, atol=1e-6), (k, np.max(np.abs(res[k][0] - res[k][1])))
+        assert abs(res["omega"][0] - res["omega"][1]) < 1e-6
 
     _run_pair(oracle_mod, N, 0.1, 0.002, 0, 1.0, loops, 987654321, 5, f0, inject=False, check=close)
 
