@@ -24,7 +24,7 @@ def main():
     from stochquant_amd import Qm1dChain
     # (N, dt, dtau, potID, loops): taumain.py presets' shapes and the C1-like chain
     for N, dt, dtau, pot, loops in [(100, 0.1, 0.002, 3, 1000), (200, 0.1, 0.002, 3, 200),
-                                    (1000, 0.05, 0.0005, 0, 1000), (4096, 0.05, 0.0005, 0, 200)]:
+                                    (1000, 0.05, 0.0005, 0, 1000), (3072, 0.05, 0.0005, 0, 200)]:
         f0 = 0.1 * np.random.default_rng(1).standard_normal(N)
         with Qm1dChain(N, dt, dtau, pot=pot, C=1.0, loops=loops, ordering="serial", lcg_seed=12345) as g:
             g.upload(f0, omega=dt * (N // 2))

@@ -4,12 +4,13 @@
 // order between barriers (oracle/orc_qm1d.c serial).
 //
 // Four launches per frame, all on one stream:
-//   gs_lcg_kernel    one wave, scalar: the LCG of tau_kernel.cl:269-284 for
-//                    every call of a full launch (rounds 0..loops-1, items
-//                    0..N), incl. the isinf retry; stores the accepted draw's
-//                    words t1>>16, t2>>16 and the seed after each call.  The
-//                    recurrence is inherently serial (the seed update is
-//                    non-linear), so this is the frame's floor.
+//   gs_lcg_kernel    one block: the LCG of tau_kernel.cl:269-284 for every
+//                    call of a full launch (rounds 0..loops-1, items 0..N),
+//                    incl. the isinf retry; stores the accepted draw's words
+//                    t1>>16, t2>>16 and the seed after each call.  The seed
+//                    update is affine mod 2^48 except on rare calls, so the
+//                    serial chain is a parallel prefix of affine maps plus an
+//                    exact serial fix-up at the exceptions (see below).
 //   gs_xi_kernel     grid-wide: xi = cos(2*3.1415*v2) * sqrt(-2 log v1) with
 //                    the reference's float casts (correctly rounded float
 //                    log/cos via fp64; glibc's logf/cosf round differently in
@@ -63,38 +64,128 @@ __device__ __forceinline__ double guard(double v) {  // :119-133
 }
 
 // ---------------------------------------------------------------- LCG ----
-__global__ __launch_bounds__(64) void gs_lcg_kernel(unsigned long long seed, int N, long long ncalls,
-                                                     uint32_t *w1, uint32_t *w2,
-                                                     unsigned long long *seeds) {
-    const uint64_t mask48 = (1ull << 48) - 1;
-    const uint64_t two31 = 2147483648ull;
-    const int lane = threadIdx.x;
-    uint64_t s = seed;
-    uint32_t a1 = 0, a2 = 0;
-    uint64_t sv = 0;
-    uint64_t g = 0;
-    for (long long k = 0; k < ncalls; ++k) {
-        uint64_t t1, t2;
-        do {  // the isinf retry of :282 fires exactly when t1 >> 16 == 0 (log(0) = -inf)
-            t1 = ((s + g) * 0x5DEECE66DULL + 0xBULL) & mask48;
-            t2 = ((t1 + g) * 0x5DEECE66DULL + 0xBULL) & mask48;
-            s = (s < two31 && t2 < two31) ? s + t2 : t2 - two31;
-        } while ((t1 >> 16) == 0);
-        const int l = (int)(k & 63);
-        if (lane == l) {
-            a1 = (uint32_t)(t1 >> 16);
-            a2 = (uint32_t)(t2 >> 16);
-            sv = s;
+// One call of random() for item g from seed s (tau_kernel.cl:269-284):
+//   t1 = (A (s+g) + B) mod 2^48,  t2 = (A (t1+g) + B) mod 2^48,
+//   s' = s + t2 if s < 2^31 and t2 < 2^31 ("case P"), else t2 - 2^31 (u64,
+//   "case Q"); repeat while t1 >> 16 == 0 (the isinf retry: log(0) = -inf).
+// In case Q, s' = alpha s + beta(g) (mod 2^48) with alpha = A^2 and
+// beta(g) = A^2 g + A B + A g + B - 2^31: affine in s.  Only s mod 2^48 and
+// the test s < 2^31 matter to later calls, and a wrapped u64 (t2 < 2^31)
+// is >= 2^31 both as u64 and mod 2^48, so the 48-bit residue carries the
+// state exactly.  Case P needs s < 2^31 AND t2 < 2^31 (about 2^-34 per call
+// after the first) and the retry 2^-32: the chain of a whole launch is a
+// composition of affine maps, evaluated by a parallel prefix, with an exact
+// serial fix-up at the (practically never taken) exceptions.
+constexpr uint64_t kM48 = (1ull << 48) - 1;
+constexpr uint64_t kLcgA = 0x5DEECE66DULL, kLcgB = 0xBULL, kTwo31 = 2147483648ull;
+constexpr uint64_t kAlpha = (kLcgA * kLcgA) & kM48;
+
+__device__ __forceinline__ uint64_t lcg_beta(uint64_t g) {
+    return (kLcgA * kLcgA * g + kLcgA * kLcgB + kLcgA * g + kLcgB - kTwo31) & kM48;
+}
+
+struct LcgCall {
+    uint64_t t1, t2, s;  // s = the seed after the call (exact u64)
+    bool exc;            // the call took case P or a retry (not the affine map)
+};
+
+__device__ __forceinline__ LcgCall lcg_case_q(uint64_t s, uint64_t g) {
+    LcgCall c;
+    c.t1 = ((s + g) * kLcgA + kLcgB) & kM48;
+    c.t2 = ((c.t1 + g) * kLcgA + kLcgB) & kM48;
+    c.exc = (c.t1 >> 16) == 0 || (s < kTwo31 && c.t2 < kTwo31);
+    c.s = c.t2 - kTwo31;
+    return c;
+}
+
+__device__ __forceinline__ LcgCall lcg_exact(uint64_t s, uint64_t g) {  // the reference's loop, verbatim semantics
+    LcgCall c;
+    do {
+        c.t1 = ((s + g) * kLcgA + kLcgB) & kM48;
+        c.t2 = ((c.t1 + g) * kLcgA + kLcgB) & kM48;
+        s = (s < kTwo31 && c.t2 < kTwo31) ? s + c.t2 : c.t2 - kTwo31;
+    } while ((c.t1 >> 16) == 0);
+    c.s = s;
+    c.exc = false;
+    return c;
+}
+
+constexpr int kLcgThreads = 1024;
+
+__global__ __launch_bounds__(kLcgThreads) void gs_lcg_kernel(unsigned long long seed, int N, long long ncalls,
+                                                              uint32_t *w1, uint32_t *w2,
+                                                              unsigned long long *seeds) {
+    __shared__ uint64_t sa[kLcgThreads], sb[kLcgThreads];
+    __shared__ long long s_exc;
+    const int t = threadIdx.x;
+    const uint64_t np1 = (uint64_t)N + 1;
+    long long k0 = 0;
+    uint64_t s_in = seed;  // exact seed before call k0
+    while (k0 < ncalls) {
+        const long long n = ncalls - k0;
+        const long long C = (n + kLcgThreads - 1) / kLcgThreads;
+        const long long kb = k0 + t * C, ke = min(ncalls, kb + C);
+        // 1. my chunk's composed case-Q map s -> a s + b (mod 2^48)
+        uint64_t a = 1, b = 0;
+        const uint64_t g0 = kb < ke ? (uint64_t)kb % np1 : 0;
+        uint64_t g = g0;
+        for (long long k = kb; k < ke; ++k) {
+            a = (kAlpha * a) & kM48;
+            b = (kAlpha * b + lcg_beta(g)) & kM48;
+            g = g + 1 == np1 ? 0 : g + 1;
         }
-        if (l == 63 || k == ncalls - 1) {
-            const long long base = k - l;
-            if (lane <= l) {
-                w1[base + lane] = a1;
-                w2[base + lane] = a2;
-                seeds[base + lane] = sv;
+        sa[t] = a;
+        sb[t] = b;
+        if (t == 0) s_exc = ncalls;
+        __syncthreads();
+        // 2. inclusive scan of the maps over threads (Hillis-Steele): after it,
+        //    (sa[t], sb[t]) = F_t o ... o F_0
+        for (int o = 1; o < kLcgThreads; o <<= 1) {
+            uint64_t pa = 1, pb = 0;
+            if (t >= o) {
+                pa = sa[t - o];
+                pb = sb[t - o];
             }
+            __syncthreads();
+            if (t >= o) {  // mine o earlier: x -> a (pa x + pb) + b
+                const uint64_t na = (sa[t] * pa) & kM48, nb = (sa[t] * pb + sb[t]) & kM48;
+                sa[t] = na;
+                sb[t] = nb;
+            }
+            __syncthreads();
         }
-        g = (g == (uint64_t)N) ? 0 : g + 1;
+        // 3. replay my chunk from its start seed (exact for chunks before the
+        //    first exception); record the first exceptional call
+        uint64_t s = t == 0 ? s_in : ((sa[t - 1] * (s_in & kM48) + sb[t - 1]) & kM48);
+        g = g0;
+        for (long long k = kb; k < ke; ++k) {
+            const LcgCall c = lcg_case_q(s, g);
+            g = g + 1 == np1 ? 0 : g + 1;
+            if (c.exc) {
+                atomicMin(&s_exc, k);
+                break;
+            }
+            w1[k] = (uint32_t)(c.t1 >> 16);
+            w2[k] = (uint32_t)(c.t2 >> 16);
+            seeds[k] = c.s;
+            s = c.s;
+        }
+        __syncthreads();
+        const long long ke0 = s_exc;
+        if (ke0 >= ncalls) break;
+        // 4. the exceptional call, exactly, then continue after it
+        if (t == 0) {
+            const uint64_t sprev = ke0 == k0 ? s_in : seeds[ke0 - 1];
+            const LcgCall c = lcg_exact(sprev, (uint64_t)ke0 % np1);
+            w1[ke0] = (uint32_t)(c.t1 >> 16);
+            w2[ke0] = (uint32_t)(c.t2 >> 16);
+            seeds[ke0] = c.s;
+            sa[0] = c.s;
+        }
+        __syncthreads();
+        s_in = sa[0];
+        k0 = ke0 + 1;
+        __syncthreads();
     }
 }
 
@@ -242,12 +333,12 @@ __device__ __forceinline__ double wave_excl_max(double v, int lane) {  // max ov
     return lane == 0 ? -__builtin_inf() : ex;
 }
 
-// LDS: f (previous step's field, the serial order's "old f"), nfc (this step),
-// x, xx0 -- 4N doubles.
+// LDS: f (previous step's field, the serial order's "old f"), n (this step),
+// d = |n - f - dw|, x, xx0 -- 5N doubles.
 __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
     extern __shared__ double lds[];
     const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
-    double *s_f = lds, *s_n = lds + N, *s_x = lds + 2 * N, *s_xx0 = lds + 3 * N;
+    double *s_f = lds, *s_n = lds + N, *s_x = lds + 2 * N, *s_xx0 = lds + 3 * N, *s_d = lds + 4 * N;
     const int lane = threadIdx.x;
     const int B = (N + 63) / 64;
     const int i0 = lane * B, i1 = min(N, i0 + B);
@@ -270,12 +361,15 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
         // the previous step's value (the persistent newf buffer at j = 0)
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
         const double T0 = nfE + xcl((double)E * a, w, pot);
-        double m1 = NEG;
+        // this step's global inputs, staged once (loads issued back to back)
+#pragma unroll 4
         for (int i = i0; i < i1; ++i) {
             const double v = row[i];
             s_n[i] = v;
-            if (i < E) m1 = fmax(m1, v + xcl((double)i * a, w, pot));
+            s_d[i] = absol(v - s_f[i] - sig * xr[i]);  // :139, |nf - f - dw|
         }
+        double m1 = NEG;
+        for (int i = i0; i < min(i1, E); ++i) m1 = fmax(m1, s_n[i] + xcl((double)i * a, w, pot));
         __syncthreads();
         const bool caseB = wave_max(m1) > T0;  // a leader before E: no reset at item E
         // lane totals of Y (X, masked below E in case A) and |X|
@@ -296,8 +390,7 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
             const double Vi = fmax(V, pa);  // V seen by item i (max over k < i)
             if (lead) {
                 last_lead = i;
-                const double d = absol(s_n[i] - s_f[i] - sig * xr[i]);
-                if (d > Vi && i < first_bad) {
+                if (s_d[i] > Vi && i < first_bad) {
                     first_bad = i;
                     Vbad = fmax(Vi, absol(X));
                 }
@@ -369,7 +462,7 @@ int qm1d_gs_block(int N) {
 
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
                               uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s) {
-    hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(64), 0, s, seed, N, ncalls, w1, w2, seeds);
+    hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(kLcgThreads), 0, s, seed, N, ncalls, w1, w2, seeds);
     const int blocks = (int)std::min<long long>(2048, (ncalls + 255) / 256);
     hipLaunchKernelGGL(gs_xi_kernel, dim3(blocks), dim3(256), 0, s, w1, w2, xi, ncalls);
     return hipGetLastError();
@@ -378,12 +471,12 @@ hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, 
 hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const int B = qm1d_gs_block(a.N);
     if (B == 0) return hipErrorInvalidValue;
-    const size_t lds1 = sizeof(double) * (size_t)a.N, lds4 = 4 * lds1;
+    const size_t lds1 = sizeof(double) * (size_t)a.N, lds5 = 5 * lds1;
     static bool attr = false;
     if (!attr) {
         hipError_t e;
         if ((e = hipFuncSetAttribute((const void *)gs_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)(4 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+                                     (int)(5 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
             return e;
         for (const void *k : {(const void *)gs_sweep_kernel<2>, (const void *)gs_sweep_kernel<8>})
             if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -393,7 +486,7 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     }
     if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(64), lds1, s, a, B);
     else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(64), lds1, s, a, B);
-    hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds4, s, a);
+    hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds5, s, a);
     return hipGetLastError();
 }
 

@@ -16,7 +16,7 @@
 // draw the reference used for its LCG seed, :185; SQ_SEED overrides).
 // SQ_ORDER=serial selects the reference's own serial order instead
 // (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
-// SQ_ORDER_SERIAL in stochquant.h), N <= 4096.
+// SQ_ORDER_SERIAL in stochquant.h), N <= 3072.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>

@@ -33,7 +33,7 @@ def _gpu_lcg(sqlib, seed, N, loops):
 
 
 @pytest.mark.parametrize("seed,N,loops", [(12345, 4, 2), (1804289383, 100, 30), (7, 3, 500),
-                                          (2 ** 31 - 3, 1000, 4)])
+                                          (2 ** 31 - 3, 1000, 4), (1804289383, 999, 1000)])
 def test_lcg_stream_matches_reference(gpu, sqlib, oracle_mod, seed, N, loops):
     xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, N, loops)
     rxi, rw1, rw2, rseeds = oracle_mod.ref_noise_stream(seed, N, loops)
@@ -82,7 +82,7 @@ def _exact(res):
 @pytest.mark.parametrize("N,loops,dtau", [(2, 3, 0.01), (3, 1, 0.01), (4, 2, 0.01), (5, 7, 0.02),
                                           (63, 20, 0.01), (64, 20, 0.01), (65, 9, 0.01), (100, 50, 0.002),
                                           (129, 13, 0.01), (200, 40, 0.004), (1000, 8, 0.001),
-                                          (4096, 3, 0.001)])
+                                          (3072, 3, 0.001)])
 def test_injected_noise_frames_bitwise_pot0(gpu, oracle_mod, N, loops, dtau):
     rng = np.random.default_rng(N)
     f0 = 0.3 * rng.standard_normal(N)
@@ -137,6 +137,28 @@ def test_double_well_within_tanh_tolerance(gpu, oracle_mod):
 
 def test_serial_order_rejects_large_n(gpu):
     from stochquant_amd import Qm1dChain, StochQuantError
-    with Qm1dChain(8192, 0.1, 0.001, pot=0, loops=2) as g:
+    with Qm1dChain(3073, 0.1, 0.001, pot=0, loops=2) as g:
         with pytest.raises(StochQuantError):
             g.set_ordering("serial")
+
+
+def test_lcg_exceptional_calls(gpu, sqlib, oracle_mod):
+    """Seeds that drive the rare branches of random(): case P (s < 2^31 and
+    t2 < 2^31 -> s + t2) and the u64 wrap of t2 - 2^31.  The parallel-prefix
+    generator's exact fix-up must reproduce the serial chain bit for bit."""
+    M = (1 << 48) - 1
+    A, B = 0x5DEECE66D, 0xB
+    found = []
+    # search small seeds whose first call has t2 < 2^31 (case P from a small seed)
+    for s in range(1, 3_000_000):
+        t1 = ((s + 0) * A + B) & M
+        t2 = ((t1 + 0) * A + B) & M
+        if t2 < 2 ** 31:
+            found.append(s)
+            if len(found) == 2:
+                break
+    assert found
+    for seed in found:
+        xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, 7, 300)
+        rxi, rw1, rw2, rseeds = oracle_mod.ref_noise_stream(seed, 7, 300)
+        assert np.array_equal(w1, rw1) and np.array_equal(w2, rw2) and np.array_equal(seeds, rseeds)
