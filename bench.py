@@ -62,7 +62,7 @@ def cpu_baseline(L, dtau, target_s):
     t0 = time.perf_counter()
     phi = oracle.phi4_step(p, phi, 0, cores)          # one step to size the sample
     t1 = time.perf_counter() - t0
-    n = max(1, min(50, int(target_s / max(t1, 1e-6))))
+    n = max(1, min(5000, int(target_s / max(t1, 1e-6))))
     t0 = time.perf_counter()
     for s in range(n):
         phi = oracle.phi4_step(p, phi, 1 + s, cores)
