@@ -14,6 +14,8 @@
 // the OpenCL platform index 2); no tau_kernel.cl is read from the cwd; the
 // kernel is Jacobi-ordered with Philox noise (seeded from the same rand()
 // draw the reference used for its LCG seed, :185; SQ_SEED overrides).
+// SQ_MODEL=phi4 (+ SQ_SHAPE, SQ_M2, SQ_LAMBDA) runs the 3-D lattice behind the
+// same arguments (run_phi4 below).
 // SQ_ORDER=serial selects the reference's own serial order instead
 // (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
 // SQ_ORDER_SERIAL in stochquant.h), N <= 3072.
@@ -76,6 +78,96 @@ int die(const char *what, sq_ctx *ctx) {
     return 1;
 }
 
+double env_double(const char *name, double dflt) {
+    const char *s = getenv(name);
+    return s ? atof(s) : dflt;
+}
+
+// SQ_MODEL=phi4: the 3-D north-star lattice behind the same 13 arguments
+// (SURVEY.md §5 "Config / flag system": extensions via env).  Shape from
+// SQ_SHAPE=LxxLyxLz (default N x N x N), V = m2/2 phi^2 + lambda/24 phi^4
+// from SQ_M2 / SQ_LAMBDA (default 1, 1); deltat and potID are unused (a = 1).
+// The printed line is the analogue of the reference's log|xavg| (the running
+// connected correlator of its chain, tauhost.c:485-501,519-521): the running
+// mean over stable frames of the zero-momentum time-slice correlator,
+// connected, log|C(t)| for t = 1..Lz-1, then Δτ and the percentage, in the
+// reference's formats, so taumain.py parses and plots it unchanged.
+// startFile / endFile are binary checkpoints (sq_load_field / sq_save_field:
+// <file> .npy + <file>.json); a resumed Δτ is capped at argv Δτ (:131-136).
+int run_phi4(int N, double deltatau, int frames, double C, int dev, int fps, int loops,
+             const char *startFile, const char *endFile, unsigned long long seed) {
+    long long L[3] = {N, N, N};
+    if (const char *sh = getenv("SQ_SHAPE")) {
+        if (sscanf(sh, "%lldx%lldx%lld", &L[0], &L[1], &L[2]) != 3) {
+            fprintf(stderr, "tauhost: SQ_SHAPE must be LxxLyxLz\n");
+            return 1;
+        }
+    }
+    sq_params p;
+    sq_params_init(&p);
+    p.model = SQ_MODEL_PHI4;
+    for (int k = 0; k < 3; ++k) p.dims[k] = L[k];
+    p.deltatau = deltatau;
+    p.C = C;
+    p.loops = loops;
+    p.seed = seed;
+    p.device = dev;
+    p.m2 = env_double("SQ_M2", 1.0);
+    p.lambda = env_double("SQ_LAMBDA", 1.0);
+    p.adapt_dtau = 1;
+    sq_ctx *ctx = nullptr;
+    if (sq_create(&p, &ctx) != SQ_OK) return die("sq_create", nullptr);
+    if (strcmp(startFile, "0") == 0) {
+        if (sq_init_field(ctx, (float)sqrt(2. * deltatau)) != SQ_OK) return die("sq_init_field", ctx);  // as :91-100
+    } else {
+        if (sq_load_field(ctx, startFile, 1) != SQ_OK) {
+            fprintf(stderr, "Failed to read Input.\n");
+            sq_destroy(ctx);
+            return 1;
+        }
+        double d = 0;
+        sq_get_dtau(ctx, &d);
+        if (d > deltatau) sq_set_dtau(ctx, deltatau);
+    }
+    const int Lz = (int)L[2];
+    const double V = (double)L[0] * (double)L[1] * (double)L[2];
+    std::vector<double> corr(Lz), cbar(Lz, 0.0);
+    double sbar = 0;  // running mean of the slice sum S(z)
+    long nstable = 0;
+    double dtautmp = 0;
+    sq_get_dtau(ctx, &dtautmp);
+    for (int j = 0; j < frames; ++j) {
+        if (j % fps == 0) {
+            for (int t = 1; t < Lz; ++t) {
+                printf(" % -.20f |", log(absol(cbar[t] - (double)Lz * sbar * sbar / V)));
+                if (t == Lz - 1) {
+                    printf("% -.20f | ", dtautmp);
+                    printf("% -.2f\n", 100. * ((double)j + 1) / (double)frames);
+                }
+            }
+        }
+        int stable = 0;
+        if (sq_run_frame(ctx, &stable) != SQ_OK) return die("sq_run_frame", ctx);
+        if (stable == 1) {
+            double m[3];
+            if (sq_correlator(ctx, corr.data(), Lz) != SQ_OK) return die("sq_correlator", ctx);
+            if (sq_moments(ctx, m) != SQ_OK) return die("sq_moments", ctx);
+            ++nstable;
+            for (int t = 0; t < Lz; ++t) cbar[t] += (corr[t] - cbar[t]) / (double)nstable;
+            sbar += (m[0] / Lz - sbar) / (double)nstable;
+        }
+        sq_get_dtau(ctx, &dtautmp);
+        fflush(stdout);
+    }
+    if (strcmp(endFile, "0") != 0 && sq_save_field(ctx, endFile) != SQ_OK) {
+        fprintf(stderr, "Failed to write to Output.\n");
+        sq_destroy(ctx);
+        return 1;
+    }
+    sq_destroy(ctx);
+    return 0;
+}
+
 }  // namespace
 
 int main(int argc, char **argv) {
@@ -101,6 +193,25 @@ int main(int argc, char **argv) {
     if (N < 2 || fps < 1 || loops < 1 || frames < 0) {
         fprintf(stderr, "tauhost: need N >= 2, fps >= 1, loops >= 1\n");
         return 1;
+    }
+    if (const char *m = getenv("SQ_MODEL")) {
+        if (strcmp(m, "phi4") == 0) {
+            unsigned long long seed = (unsigned long long)abs(rand());
+            if (const char *s = getenv("SQ_SEED")) seed = strtoull(s, nullptr, 0);
+            int ndev = 0;
+            sq_device_count(&ndev);
+            if (ndev < 1) {
+                fprintf(stderr, "tauhost: no HIP device\n");
+                return 1;
+            }
+            if (const char *s = getenv("SQ_DEVICE")) dev = atoi(s);
+            dev = ((dev % ndev) + ndev) % ndev;
+            return run_phi4(N, deltatau, frames, C, dev, fps, loops, startFile, endFile, seed);
+        }
+        if (strcmp(m, "qm1d") != 0) {
+            fprintf(stderr, "tauhost: SQ_MODEL must be qm1d or phi4\n");
+            return 1;
+        }
     }
     const int midpt = N / 2;
     int recSimlgth = 0;

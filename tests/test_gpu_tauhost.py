@@ -151,3 +151,39 @@ def test_serial_order_all_unstable_preset(gpu, tmp_path):
     tail = end.strip().split("\n")[-3:]
     assert float(tail[2].split("|")[0]) == pytest.approx(g["end_dtau"], rel=1e-6)
     assert int(tail[1].split("|")[0]) == g["end_N"]
+
+
+def test_phi4_mode_through_the_cli(gpu, tmp_path):
+    """SQ_MODEL=phi4: the 3-D lattice behind the reference's 13 arguments.
+    stdout is taumain-parseable (Lz-1 values, dtau, percent; first frame -inf
+    like the reference's), the end file is a binary checkpoint, a START resume
+    continues the noise stream bit for bit, and the field equals the library
+    run with the same seed."""
+    from stochquant_amd import Phi4Lattice, parse_frame_line
+    env = dict(SQ_MODEL="phi4", SQ_SHAPE="64x16x32", SQ_SEED="7", SQ_M2="0.5", SQ_LAMBDA="1.5")
+    argv = lambda frames, start: ["32", "1", "0.01", str(frames), "0", "1", "0", "1", "0", "10", start, "END", "12"]
+    out, _ = _run_env(tmp_path, argv(4, "0"), **env)
+    lines = out.strip().split("\n")
+    assert len(lines) == 4
+    for k, ln in enumerate(lines):
+        r = parse_frame_line(ln.encode())
+        assert r["y"].size == 31 and r["dtau"] == pytest.approx(0.01) and r["percent"] == pytest.approx(25 * (k + 1))
+    assert np.all(np.isneginf(parse_frame_line(lines[0].encode())["y"]))
+    assert np.all(np.isfinite(parse_frame_line(lines[-1].encode())["y"]))
+    full = np.load(tmp_path / "end")
+    import json
+    meta = json.loads((tmp_path / "end.json").read_text())
+    assert full.shape == (32, 16, 64) and meta["step"] == 40 and meta["dims"] == [64, 16, 32]
+    # resume: 2 frames, then 2 more from the checkpoint
+    d2 = tmp_path / "r"
+    d2.mkdir()
+    _run_env(d2, argv(2, "0"), **env)
+    shutil.copy(d2 / "end", d2 / "start")
+    shutil.copy(d2 / "end.json", d2 / "start.json")
+    _run_env(d2, argv(2, "START"), **env)
+    assert np.array_equal(np.load(d2 / "end"), full)
+    with Phi4Lattice((64, 16, 32), dtau=0.01, m2=0.5, lam=1.5, seed=7, loops=10) as L:
+        L.init_field(float(np.float32(np.sqrt(2 * 0.01))))
+        for _ in range(4):
+            assert L.run_frame()
+        assert np.array_equal(L.download(), full)
