@@ -389,7 +389,7 @@ int create_phi4(sq_ctx *c) {
     }
     if (const char *e = getenv("SQ_VSEG"))  // tuning override: float4 segments per lane
         if (atoi(e) == 1 || (atoi(e) == 2 && c->geom.qx == 64 && c->Lx % 512 == 0)) c->geom.v = atoi(e);
-    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = atoi(e) == 2 ? 2 : 1;
+    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = atoi(e) == 2 ? 2 : atoi(e) == 3 ? 3 : 1;
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;

@@ -35,7 +35,8 @@ struct Phi4Geom {
     int qx;   // lanes per x segment (4 sites each)
     int r;    // rows per lane
     int wy;   // rows per wave unit
-    int pf;   // z prefetch distance of the register queue (1 or 2; 2 only for qx == 64, v == 1)
+    int pf;   // register queue: 1 prefetch distance 1; 2 distance 2 (qx == 64, v == 1);
+              // 3 distance 1 + packed-f32 site arithmetic (qx == 64, the default there)
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 

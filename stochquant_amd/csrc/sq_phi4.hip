@@ -86,6 +86,35 @@ __device__ __forceinline__ float site_update(float phi, float xm, float xp, floa
     return fmaxf(fminf(v, A.clampv), -A.clampv);
 }
 
+// The same update for the 4 sites of a float4 with packed f32 arithmetic
+// (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 on site pairs): identical
+// operations and order per site, so bit-identical results; the x-neighbour
+// sums stay scalar (their operands are not register-pair aligned).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <bool NZ>
+__device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, float4 up, float4 dn,
+                                               float4 zm, float4 zp, const f32x4n &xi,
+                                               const Phi4StepArgs &A) {
+    const f32x2 c0 = {c.x, c.y}, c1 = {c.z, c.w};
+    const f32x2 x0 = {lft + c.y, c.x + c.z}, x1 = {c.y + c.w, c.z + rgt};
+    const f32x2 y0 = f32x2{up.x, up.y} + f32x2{dn.x, dn.y}, y1 = f32x2{up.z, up.w} + f32x2{dn.z, dn.w};
+    const f32x2 z0 = f32x2{zm.x, zm.y} + f32x2{zp.x, zp.y}, z1 = f32x2{zm.z, zm.w} + f32x2{zp.z, zp.w};
+    const f32x2 nb0 = (x0 + y0) + z0, nb1 = (x1 + y1) + z1;
+    const f32x2 m6 = {-6.0f, -6.0f}, l6 = {A.lam6, A.lam6}, m2 = {A.m2, A.m2}, h = {A.h, A.h};
+    const f32x2 lap0 = __builtin_elementwise_fma(m6, c0, nb0), lap1 = __builtin_elementwise_fma(m6, c1, nb1);
+    const f32x2 g0 = __builtin_elementwise_fma(l6, c0 * c0, m2), g1 = __builtin_elementwise_fma(l6, c1 * c1, m2);
+    const f32x2 d0 = __builtin_elementwise_fma(-c0, g0, lap0), d1 = __builtin_elementwise_fma(-c1, g1, lap1);
+    f32x2 v0 = __builtin_elementwise_fma(h, d0, c0), v1 = __builtin_elementwise_fma(h, d1, c1);
+    if (NZ) {
+        const f32x2 sg = {A.sig, A.sig};
+        v0 = __builtin_elementwise_fma(sg, f32x2{xi.a, xi.b}, v0);
+        v1 = __builtin_elementwise_fma(sg, f32x2{xi.c, xi.d}, v1);
+    }
+    const float cl = A.clampv;
+    return make_float4(fmaxf(fminf(v0.x, cl), -cl), fmaxf(fminf(v0.y, cl), -cl), fmaxf(fminf(v1.x, cl), -cl),
+                       fmaxf(fminf(v1.y, cl), -cl));
+}
+
 // Philox4x32-10 on R independent counters, round-major so the R dependency
 // chains interleave; the three-input xors are one v_bitop3_b32 each.
 template <int R>
@@ -145,7 +174,7 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
@@ -212,10 +241,14 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
                 if (v == V - 1 && L.lane == 63) rgt = er[r];
             }
             float4 o;
-            o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[k].x, N.row[k].x, xi[k].a, A);
-            o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[k].y, N.row[k].y, xi[k].b, A);
-            o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[k].z, N.row[k].z, xi[k].c, A);
-            o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[k].w, N.row[k].w, xi[k].d, A);
+            if constexpr (PK) {
+                o = site_update4<NZ>(cc, lft, rgt, up, dn, P.row[k], N.row[k], xi[k], A);
+            } else {
+                o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[k].x, N.row[k].x, xi[k].a, A);
+                o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[k].y, N.row[k].y, xi[k].b, A);
+                o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[k].z, N.row[k].z, xi[k].c, A);
+                o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[k].w, N.row[k].w, xi[k].d, A);
+            }
             const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
             bad |= (int)(m >= A.clampv);
             if (L.rows_ok) bstore4(ws, L.voff[k], o);
@@ -224,13 +257,13 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
                                            uint32_t qplane, int &bad) {
     load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, PK>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
@@ -241,7 +274,7 @@ __device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX
                                             const Slot<R, V> &N, Slot<R, V> &F, int z, int zend,
                                             size_t plane, uint32_t pbytes, uint32_t qplane, int &bad) {
     if (z + 2 <= zend) load_slot<QX, R, V>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, false>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 template <int QX, int R, int V, bool MS, bool NZ, int PF>
@@ -300,14 +333,16 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     load_slot<QX, R, V>(A, L, S0, zbeg - 1, false, plane, pbytes);
     load_slot<QX, R, V>(A, L, S1, zbeg, true, plane, pbytes);
     int bad = 0;
-    if constexpr (PF == 1) {
+    if constexpr (PF != 2) {
         // three-slot register queue, unrolled so no rotation moves are needed
+        // (PF == 3: same queue, packed-f32 site arithmetic)
+        constexpr bool PK = PF == 3;
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
         }
     } else {
         // four-slot queue, prefetch distance 2
@@ -420,17 +455,21 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     // Measured (profiles/r01/sweep*): 256-wide rows (256^3 is MALL-resident)
     // want R = 1, zc = 4; 512-wide and wider rows (HBM-bound) want R = 2, zc = 8.
     const int v = (qx == 64 && Lx % 512 == 0) ? 2 : 1;
+    // full-row waves use packed-f32 site arithmetic (queue mode 3): bit-identical,
+    // 15 % fewer VALU instructions, measured 256^3 22.3 -> 21.3 us, 512^3
+    // 196.5 -> 193.4 us (profiles/r01/sweep*_packed.log)
+    const int pf = qx == 64 ? 3 : 1;
     const bool narrow = Lx <= 256;
     const int rcand[3] = {narrow ? 1 : 2, narrow ? 2 : 4, narrow ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
         if (Ly % (rs * r) == 0) {
-            *g = Phi4Geom{qx, r, rs * r, 1, v};
+            *g = Phi4Geom{qx, r, rs * r, pf, v};
             return true;
         }
     }
     for (int r : rcand) {  // otherwise a partial last tile (rows past Ly idle)
         if (Ly % r == 0) {
-            *g = Phi4Geom{qx, r, rs * r, 1, v};
+            *g = Phi4Geom{qx, r, rs * r, pf, v};
             return true;
         }
     }
@@ -460,6 +499,11 @@ static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hi
         if (pf == 2)
             return nz ? launch_pf<QX, R, V, MS, true, 2>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 2>(a, grid, s, e0, e1);
+    }
+    if constexpr (QX == 64) {
+        if (pf == 3)
+            return nz ? launch_pf<QX, R, V, MS, true, 3>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 3>(a, grid, s, e0, e1);
     }
     return nz ? launch_pf<QX, R, V, MS, true, 1>(a, grid, s, e0, e1)
               : launch_pf<QX, R, V, MS, false, 1>(a, grid, s, e0, e1);
