@@ -119,6 +119,7 @@ struct sq_ctx {
     std::vector<Slab> slabs;
     int cur = 0;
     int *flag = nullptr;
+    bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;
     ncclComm_t comm = nullptr;
@@ -203,7 +204,7 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.k1 = (uint32_t)(c->p.seed >> 32);
     a.s_lo = (uint32_t)c->step;
     a.s_hi = (uint32_t)(c->step >> 32);
-    a.flag = c->flag;
+    a.flag = c->in_frame ? c->flag : nullptr;  // the guard flag only feeds a frame's rollback
     return a;
 }
 
@@ -673,7 +674,9 @@ int phi4_frame(sq_ctx *c, int *stable) {
     SQ_HIP(hipMemsetAsync(c->flag, 0, sizeof(int), c->slabs[0].sA));
     rc = phi4_join(c);
     if (rc) return rc;
+    c->in_frame = true;
     rc = phi4_steps(c, c->p.loops);
+    c->in_frame = false;
     if (rc) return rc;
     rc = phi4_join(c);
     if (rc) return rc;

@@ -249,8 +249,10 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
                 o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[k].z, N.row[k].z, xi[k].c, A);
                 o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[k].w, N.row[k].w, xi[k].d, A);
             }
-            const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-            bad |= (int)(m >= A.clampv);
+            if (A.flag != nullptr) {  // frames only: raw sq_step has no rollback to feed
+                const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+                bad |= (int)(m >= A.clampv);
+            }
             if (L.rows_ok) bstore4(ws, L.voff[k], o);
         }
     }
