@@ -160,7 +160,8 @@ int sq_set_step(sq_ctx *ctx, unsigned long long step);
 /* Correlator of the reference's observables: QM1D out[i] = xx0[i] -
  * x[i]*x[mid] (host xavg, tauhost.c:519-521), n <= N.  PHI4: zero-momentum
  * time-slice correlator over z, out[t] = <S(z) S(z+t)>/V, n <= Lz, where
- * S(z) = sum_{x,y} phi (single-slab contexts). */
+ * S(z) = sum_{x,y} phi over the whole lattice (slab contexts: one RCCL sum
+ * all-reduce of the slice sums; collective, every rank must call it). */
 int sq_correlator(sq_ctx *ctx, double *out, int n);
 
 /* Profiling of the step kernels on their stream: mode 1 = every launch timed

@@ -1077,24 +1077,33 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
         for (int i = 0; i < n; ++i) out[i] = xx0[i] - x[i] * x[mid];  // tauhost.c:519-521
         return SQ_OK;
     }
-    if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1)
-        return fail(SQ_E_STATE, "slice correlator needs the whole lattice in this process");
     if (n > c->Lz) return fail(SQ_E_ARG, "n > Lz");
     int rc = phi4_join(c);
     if (rc) return rc;
-    std::vector<double> S;
-    double *d = nullptr;
-    for (auto &s : c->slabs) {
-        SQ_HIP(hipMalloc(&d, sizeof(double) * s.nz));
-        hipError_t e = sq::phi4_slices_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, d, s.sA);
-        std::vector<double> h(s.nz);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
-        if (e == hipSuccess) e = hipMemcpy(h.data(), d, sizeof(double) * s.nz, hipMemcpyDeviceToHost);
-        (void)hipFree(d);
-        if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
-        S.insert(S.end(), h.begin(), h.end());
-    }
+    // slice sums S(z) of the whole lattice: every slab writes its planes into a
+    // zeroed global-length array; across ranks one RCCL sum all-reduce (the
+    // per-frame collective of SURVEY.md §8e)
     const long long Lz = c->Lz;
+    std::vector<double> S((size_t)Lz, 0.0);
+    double *d = nullptr;
+    SQ_HIP(hipMalloc(&d, sizeof(double) * (size_t)Lz));
+    hipStream_t s0 = c->slabs[0].sA;
+    hipError_t e = hipMemsetAsync(d, 0, sizeof(double) * (size_t)Lz, s0);
+    for (auto &s : c->slabs) {
+        if (e == hipSuccess) e = hipStreamSynchronize(s0);
+        if (e == hipSuccess) e = sq::phi4_slices_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, d + s.z0, s.sA);
+        if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
+    }
+    if (e == hipSuccess && c->p.comm == SQ_COMM_RCCL && c->comm != nullptr) {
+        if (ncclAllReduce(d, d, (size_t)Lz, ncclFloat64, ncclSum, c->comm, s0) != ncclSuccess) {
+            (void)hipFree(d);
+            return fail(SQ_E_COMM, "ncclAllReduce of the slice sums failed");
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s0);
+    if (e == hipSuccess) e = hipMemcpy(S.data(), d, sizeof(double) * (size_t)Lz, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
     const double vol = (double)c->Lx * c->Ly * (double)Lz;
     for (int t = 0; t < n; ++t) {
         double acc = 0;

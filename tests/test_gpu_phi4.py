@@ -294,3 +294,24 @@ def test_checkpoint_roundtrip_resumes_noise_bitwise(gpu, oracle_mod, tmp_path):
         from stochquant_amd import StochQuantError
         with pytest.raises(StochQuantError):
             L.load(tmp_path / "ck.npy")
+
+
+def test_slice_correlator_across_slabs(gpu, oracle_mod):
+    """The zero-momentum correlator of a decomposed lattice (loopback slabs;
+    RCCL self-exchange = the all-reduce code path of the multi-rank case) equals
+    the single-slab one exactly: per-plane sums are the same kernels."""
+    from stochquant_amd import unique_id
+    shape = (64, 16, 24)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(3)
+        mono = L.correlator(24)
+    with _lat(shape, comm="loopback", nslabs=3) as L:
+        L.upload(phi0)
+        L.step(3)
+        assert np.array_equal(L.correlator(24), mono)
+    with _lat(shape, comm="rccl", nranks=1, rank=0, comm_id=unique_id()) as L:
+        L.upload(phi0)
+        L.step(3)
+        assert np.array_equal(L.correlator(24), mono)
