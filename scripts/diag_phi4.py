@@ -19,11 +19,13 @@ def main():
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--C", type=float, default=1.0)
+    ap.add_argument("--sizes", default="", help="copy: buffer sizes in MiB (comma list)")
     a = ap.parse_args()
     from stochquant_amd import Phi4Lattice, _lib
     lib = _lib.load()
     if a.what == "copy":
-        for mib in (16, 32, 64, 96, 128, 256, 512, 1024, 2048):
+        sizes = [int(v) for v in a.sizes.split(",")] if a.sizes else [16, 32, 64, 96, 128, 256, 512, 1024, 2048]
+        for mib in sizes:
             g = ctypes.c_double()
             iters = max(10, int(20 * 1024 / mib))
             rc = lib.sq_copy_bandwidth(0, mib << 20, iters, ctypes.byref(g))

@@ -460,9 +460,13 @@ int create_phi4(sq_ctx *c) {
     const long long rows = (long long)(c->Lx / (4 * c->geom.qx * c->geom.v)) * (c->Ly / c->geom.wy);
     const int nz_max = c->slabs[0].nz;
     // measured optima (profiles/r01/sweep*): zc = 4 for one-segment rows (256^3),
-    // zc = 8 when rows span several 256-site segments (512^3)
+    // zc = 8 when rows span several 256-site segments (512^3); big lattices
+    // lengthen the chunk while >= 32 waves per SIMD remain, which cuts the
+    // chunk-edge plane re-reads (1024^3: zc 32, 1760 -> 1711 us,
+    // profiles/r01/sweep1024_zc.log)
     int zc = c->Lx > 256 ? 8 : 4;
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
+    while (zc < 32 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 32768) zc *= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     c->zc = zc;
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream

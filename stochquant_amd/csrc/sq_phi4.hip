@@ -287,10 +287,13 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
     const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
     if (unit >= A.nunits) return;
-    const int yg = unit % A.nyg;
-    const int rest = unit / A.nyg;
-    const int xs = rest % A.nxseg;
-    const int zk = rest / A.nxseg;
+    // x-segments fastest, then y-groups: the waves that share a row's segment
+    // edges (MS) and the y-halo rows are consecutive units, i.e. the same or
+    // the adjacent block on the same XCD, so those lines are L2 hits
+    const int xs = unit % A.nxseg;
+    const int rest = unit / A.nxseg;
+    const int yg = rest % A.nyg;
+    const int zk = rest / A.nyg;
     const int zbeg = A.zlo + zk * A.zstep;
     const int zend = min(zbeg + A.zc, A.zhi);
 
