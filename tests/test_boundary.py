@@ -82,3 +82,14 @@ def test_frame_line_parser_matches_taumain():
     r = parse_frame_line(b" -inf | -inf | -inf | 0.01000000000000000021 |  50.00\n")
     assert list(r["y"]) == [float("-inf")] * 3
     assert r["dtau"] == 0.01 and r["percent"] == 50.0
+
+
+def test_driver_presets_mirror_taumain():
+    """stochquant_amd.driver.PRESETS / preset_argv = taumain.py:91-132."""
+    from stochquant_amd.driver import PRESETS, preset_argv
+    assert PRESETS["double_well"] == {"dtau": .002, "Nt": 200, "dt": .02, "potID": 3, "theoVal": 10, "c": 1.,
+                                      "filename": "V0_2e_0-8.txt"}
+    assert PRESETS["harmosc"]["dtau"] == .3 and PRESETS["harmosc"]["Nt"] == 100
+    argv = preset_argv("double_well", exe="./tauhost.o")
+    assert argv == ["./tauhost.o", "200", "0.02", "0.002", "5000", "3", "1.0", "2", "1", "0", "1000", "0",
+                    "V0_2e_0-8.txt", "40"]

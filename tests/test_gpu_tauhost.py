@@ -189,3 +189,19 @@ def test_phi4_mode_through_the_cli(gpu, tmp_path):
         for _ in range(4):
             assert L.run_frame()
         assert np.array_equal(L.download(), full)
+
+
+def test_taumain_driver_double_well(gpu, tmp_path):
+    """The taumain.py flow headless (stochquant_amd.driver): spawn, stream,
+    parse; 199 values per frame, percent ends at 100, end file written."""
+    from stochquant_amd.driver import TauhostRun
+    frames = []
+    with TauhostRun("double_well", frames=6, loops=200, cwd=str(tmp_path)) as run:
+        for fr in run:
+            frames.append(fr)
+    assert run.returncode == 0, run.stderr
+    assert len(frames) == 6 and frames[-1]["percent"] == pytest.approx(100.0)
+    y = frames[-1]["y"]
+    assert np.all(np.isfinite(y) | np.isneginf(y))   # -inf while no frame was stable yet (Δτ/Δt² = 5)
+    assert frames[-1]["dtau"] <= 0.002
+    assert (tmp_path / "V0_2e_0-8.txt").exists()
