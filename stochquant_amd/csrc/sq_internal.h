@@ -36,7 +36,8 @@ struct Phi4Geom {
     int r;    // rows per lane
     int wy;   // rows per wave unit
     int pf;   // register queue: 1 prefetch distance 1; 2 distance 2 (qx == 64, v == 1);
-              // 3 distance 1 + packed-f32 site arithmetic (qx == 64, the default there)
+              // 3 distance 1 + packed-f32 site arithmetic (qx == 64, the default there);
+              // 4 as 3 with non-temporal output stores (default when the fields exceed the MALL)
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 

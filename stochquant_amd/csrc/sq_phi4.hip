@@ -47,9 +47,10 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off)
     const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_float4(v.x, v.y, v.z, v.w);
 }
+template <int AUX = 0>
 __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
     const f32x4v w = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
 }
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
@@ -174,7 +175,7 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
@@ -253,19 +254,19 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
                 const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
                 bad |= (int)(m >= A.clampv);
             }
-            if (L.rows_ok) bstore4(ws, L.voff[k], o);
+            if (L.rows_ok) bstore4<SAUX>(ws, L.voff[k], o);
         }
     }
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
                                            uint32_t qplane, int &bad) {
     load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
@@ -341,13 +342,19 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     if constexpr (PF != 2) {
         // three-slot register queue, unrolled so no rotation moves are needed
         // (PF == 3: same queue, packed-f32 site arithmetic)
-        constexpr bool PK = PF == 3;
+        constexpr bool PK = PF >= 3;
+        // PF == 4: non-temporal output stores, for lattices whose two fields
+        // exceed the Infinity Cache (the output is not re-read this step, and
+        // keeping it out of L2/MALL leaves them to the input's halo reuse):
+        // 512^3 199.7 -> 186.8 us, 1024^3 1606 -> 1570 us; at 256^3 (MALL-
+        // resident) it costs 21.6 -> 30.0 us (profiles/r01/sweep*_ntstore.log)
+        constexpr int SAUX = PF == 4 ? 2 : 0;
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ, PK>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
         }
     } else {
         // four-slot queue, prefetch distance 2
@@ -509,6 +516,9 @@ static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hi
         if (pf == 3)
             return nz ? launch_pf<QX, R, V, MS, true, 3>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 3>(a, grid, s, e0, e1);
+        if (pf == 4)
+            return nz ? launch_pf<QX, R, V, MS, true, 4>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 4>(a, grid, s, e0, e1);
     }
     return nz ? launch_pf<QX, R, V, MS, true, 1>(a, grid, s, e0, e1)
               : launch_pf<QX, R, V, MS, false, 1>(a, grid, s, e0, e1);
