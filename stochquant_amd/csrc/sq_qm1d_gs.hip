@@ -472,7 +472,11 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const int B = qm1d_gs_block(a.N);
     if (B == 0) return hipErrorInvalidValue;
     const size_t lds1 = sizeof(double) * (size_t)a.N, lds5 = 5 * lds1;
-    static bool attr = false;
+    // the dynamic-LDS limit is a per-device function attribute: set it once per device
+    static bool attr_set[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    bool &attr = attr_set[dev];
     if (!attr) {
         hipError_t e;
         if ((e = hipFuncSetAttribute((const void *)gs_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
