@@ -71,7 +71,7 @@ class TauhostRun:
         if not os.path.exists(self.argv[0]):
             raise _lib.StochQuantUnavailable(f"{self.argv[0]} not built")
         self.proc = subprocess.Popen(self.argv, cwd=self.cwd, env=self.env, stdout=subprocess.PIPE,
-                                     stderr=subprocess.PIPE, bufsize=1)
+                                     stderr=subprocess.PIPE, bufsize=0)
         self._t = threading.Thread(target=self._reader, daemon=True)
         self._t.start()
         return self
