@@ -19,8 +19,6 @@ import subprocess
 import threading
 from queue import Queue
 
-import numpy as np
-
 from . import _lib
 from .langevin import parse_frame_line, tauhost_argv
 
