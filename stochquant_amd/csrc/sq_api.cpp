@@ -66,6 +66,7 @@ struct Slab {
     long long z0 = 0;
     hipStream_t sA = nullptr, sB = nullptr;
     hipEvent_t evA = nullptr, evC = nullptr;  // A: block's steps done; C: its halo exchange done
+    hipEvent_t evE = nullptr;                 // E: the block's output edge planes (what the next exchange sends) done
 };
 
 struct EvPair {
@@ -120,6 +121,7 @@ struct sq_ctx {
     int cur = 0;
     int *flag = nullptr;
     bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
+    bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;
     ncclComm_t comm = nullptr;
@@ -258,7 +260,10 @@ int phi4_periodic_step(sq_ctx *c) {
 //   stream A: step 0 on the planes that need no ghost, [1, nz-1), overlapped
 //             with the exchange; then (after evC) step 0 on the rim
 //             [-(g-1), 1) u [nz-1, nz+g-1); then steps s = 1..g-1 on the
-//             shrinking extended range [-(g-1-s), nz+g-1-s); record evA.
+//             shrinking extended range [-(g-1-s), nz+g-1-s); the last step
+//             computes its edge planes [0, G) u [nz-G, nz) first and records
+//             evE, so the NEXT block's exchange overlaps this step's middle
+//             as well as the next core; record evA.
 // Ghost-zone sites are recomputed redundantly; the counter-based noise makes
 // them bit-identical to their owner's, so the result equals the monolithic run.
 int phi4_block(sq_ctx *c, int g) {
@@ -269,10 +274,10 @@ int phi4_block(sq_ctx *c, int g) {
     // 1. exchange (stream B)
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        SQ_HIP(hipStreamWaitEvent(s.sB, s.evA, 0));
+        SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
         if (c->p.comm == SQ_COMM_LOOPBACK) {  // we write the neighbours' ghosts: wait for them too
-            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evA, 0));
-            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evA, 0));
+            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evE, 0));
+            SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evE, 0));
         }
     }
     if (c->p.comm == SQ_COMM_LOOPBACK) {
@@ -327,16 +332,32 @@ int phi4_block(sq_ctx *c, int g) {
         if (rc) return rc;
     }
     count_step(c);
-    // 4. steps 1..g-1 on the shrinking extended range
+    // 4. steps 1..g-1 on the shrinking extended range; the last one edges first
+    bool edges_recorded = false;
     for (int st = 1; st < g; ++st) {
         const int in_buf = cur ^ (st & 1);
+        const bool split = st == g - 1;
         for (auto &s : c->slabs) {
-            int rc = phi4_launch_span(c, s, in_buf, s.sA, -(g - 1 - st), s.nz + (g - 1 - st), true);
+            int rc;
+            if (split && c->edge_first && s.nz > 2 * G) {
+                rc = phi4_launch_span(c, s, in_buf, s.sA, 0, G, true);
+                if (rc) return rc;
+                rc = phi4_launch_span(c, s, in_buf, s.sA, s.nz - G, s.nz, false);
+                if (rc) return rc;
+                SQ_HIP(hipEventRecord(s.evE, s.sA));
+                rc = phi4_launch_span(c, s, in_buf, s.sA, G, s.nz - G, false);
+                edges_recorded = true;
+            } else {
+                rc = phi4_launch_span(c, s, in_buf, s.sA, -(g - 1 - st), s.nz + (g - 1 - st), true);
+            }
             if (rc) return rc;
         }
         count_step(c);
     }
-    for (auto &s : c->slabs) SQ_HIP(hipEventRecord(s.evA, s.sA));
+    for (auto &s : c->slabs) {
+        SQ_HIP(hipEventRecord(s.evA, s.sA));
+        if (!edges_recorded) SQ_HIP(hipEventRecord(s.evE, s.sA));
+    }
     c->cur = cur ^ (g & 1);
     return SQ_OK;
 }
@@ -446,8 +467,10 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipStreamCreateWithPriority(&s.sB, hipStreamNonBlocking, prio_hi));
         SQ_HIP(hipEventCreateWithFlags(&s.evA, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evC, hipEventDisableTiming));
+        SQ_HIP(hipEventCreateWithFlags(&s.evE, hipEventDisableTiming));
         SQ_HIP(hipEventRecord(s.evA, s.sA));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
+        SQ_HIP(hipEventRecord(s.evE, s.sA));
         c->slabs.push_back(s);
     }
     SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
@@ -473,6 +496,7 @@ int create_phi4(sq_ctx *c) {
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     while (zc < 32 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 32768) zc *= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
+    if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
     c->zc = zc;
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
@@ -788,6 +812,7 @@ int sq_destroy(sq_ctx *c) {
         if (s.sB) (void)hipStreamDestroy(s.sB);
         if (s.evA) (void)hipEventDestroy(s.evA);
         if (s.evC) (void)hipEventDestroy(s.evC);
+        if (s.evE) (void)hipEventDestroy(s.evE);
     }
     for (int k = 0; k < 2; ++k) {
         (void)hipFree(c->qf[k]);
