@@ -416,7 +416,7 @@ int create_phi4(sq_ctx *c) {
         const double field_bytes = 4.0 * c->Lx * c->Ly * (double)nz_dev;  // this device's share
         if (c->geom.pf == 3 && 2.0 * field_bytes > 192.0 * (1 << 20)) c->geom.pf = 4;
     }
-    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = (atoi(e) >= 1 && atoi(e) <= 4) ? atoi(e) : 1;
+    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = (atoi(e) >= 1 && atoi(e) <= 5) ? atoi(e) : 1;
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;

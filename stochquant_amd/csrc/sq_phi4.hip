@@ -153,6 +153,9 @@ struct Lane {
     uint32_t qoff[R * V];   // Philox quad offset inside the plane
     bool rows_ok;
     int lane;
+    int w;                  // wave in the block
+    int hmask;              // halo rows this wave loads from memory: bit 0 y-1, bit 1 y+R
+    float4 *lds;            // LH: the block's boundary-row exchange buffer
 };
 
 template <int QX, int R, int V>
@@ -165,8 +168,8 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
     if (halo) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-            s.hm[v] = bload4(rs, L.vm[v]);
-            s.hp[v] = bload4(rs, L.vp[v]);
+            if (L.hmask & 1) s.hm[v] = bload4(rs, L.vm[v]);
+            if (L.hmask & 2) s.hp[v] = bload4(rs, L.vp[v]);
         }
     }
 }
@@ -175,7 +178,7 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
@@ -208,6 +211,36 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 #pragma unroll
         for (int k = 0; k < R * V; ++k) xi[k] = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
+    // y-halo rows: from memory, or (LH, queue mode 5, SQ_PREFETCH=5) the 4 y-adjacent waves of the block
+    // publish their first / last rows in LDS and only the block's two outer
+    // halo rows come from memory (double-buffered by plane parity: one barrier
+    // per plane keeps the waves within one plane of each other).  Measured
+    // (profiles/r01/sweep*_lds_halo.log): halves the L2 requests but the
+    // per-plane barrier costs more than the L2 hits it saves -- 256^3 20.8 ->
+    // 21.6 us, 512^3 unchanged -- so the default reads halos from L2.
+    float4 hmv[V], hpv[V];
+    if constexpr (LH) {
+        float4 *mine = L.lds + ((z & 1) * 4 + L.w) * 2 * V * 64;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            mine[v * 64 + L.lane] = C.row[v];
+            mine[(V + v) * 64 + L.lane] = C.row[(R - 1) * V + v];
+        }
+        __syncthreads();
+        const float4 *up_w = L.lds + ((z & 1) * 4 + L.w - 1) * 2 * V * 64;
+        const float4 *dn_w = L.lds + ((z & 1) * 4 + L.w + 1) * 2 * V * 64;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            hmv[v] = L.w == 0 ? C.hm[v] : up_w[(V + v) * 64 + L.lane];
+            hpv[v] = L.w == 3 ? C.hp[v] : dn_w[v * 64 + L.lane];
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            hmv[v] = C.hm[v];
+            hpv[v] = C.hp[v];
+        }
+    }
     const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, A.periodic ? z + 1 : z + A.gz, plane, pbytes);
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -230,8 +263,8 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         for (int v = 0; v < V; ++v) {
             const int k = r * V + v;
             const float4 cc = C.row[k];
-            const float4 up = r > 0 ? C.row[r > 0 ? k - V : 0] : C.hm[v];
-            const float4 dn = r < R - 1 ? C.row[r < R - 1 ? k + V : 0] : C.hp[v];
+            const float4 up = r > 0 ? C.row[r > 0 ? k - V : 0] : hmv[v];
+            const float4 dn = r < R - 1 ? C.row[r < R - 1 ? k + V : 0] : hpv[v];
             float lft = rl[v], rgt = rr[v];
             if constexpr (V > 1) {
                 if (L.lane == 0) lft = rl[(v + V - 1) % V];
@@ -260,13 +293,13 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
                                            uint32_t qplane, int &bad) {
     load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK, SAUX>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
@@ -304,6 +337,11 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     const uint32_t qplane = (uint32_t)(plane >> 2);
     Lane<QX, R, V> L;
     L.lane = threadIdx.x & 63;
+    L.w = (int)(threadIdx.x >> 6);
+    constexpr bool LH = PF == 5;
+    __shared__ float4 s_halo[LH ? 2 * 4 * 2 * V * 64 : 1];
+    L.lds = s_halo;
+    L.hmask = LH ? ((L.w == 0 ? 1 : 0) | (L.w == 3 ? 2 : 0)) : 3;
     const int xq = L.lane & (QX - 1);
     const int rsid = L.lane / QX;
     const int xspan = xs * (4 * QX * V);     // first site of this wave's x-span
@@ -350,11 +388,11 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
         // resident) it costs 21.6 -> 30.0 us (profiles/r01/sweep*_ntstore.log)
         constexpr int SAUX = PF == 4 ? 2 : 0;
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
         }
     } else {
         // four-slot queue, prefetch distance 2
@@ -519,6 +557,15 @@ static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hi
         if (pf == 4)
             return nz ? launch_pf<QX, R, V, MS, true, 4>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 4>(a, grid, s, e0, e1);
+        // LH needs each block's 4 waves to be 4 y-adjacent groups of one z-chunk
+        if constexpr (!MS) {
+            if (pf == 5 && a.nxseg == 1 && a.nyg % 4 == 0)
+                return nz ? launch_pf<QX, R, V, MS, true, 5>(a, grid, s, e0, e1)
+                          : launch_pf<QX, R, V, MS, false, 5>(a, grid, s, e0, e1);
+        }
+        if (pf == 5)
+            return nz ? launch_pf<QX, R, V, MS, true, 3>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 3>(a, grid, s, e0, e1);
     }
     return nz ? launch_pf<QX, R, V, MS, true, 1>(a, grid, s, e0, e1)
               : launch_pf<QX, R, V, MS, false, 1>(a, grid, s, e0, e1);
