@@ -136,6 +136,11 @@ int sq_slab(sq_ctx *ctx, long long *nz_local, long long *z0);
 /* PHI4 register tile of the step kernel: out = {lanes per x segment, rows
  * per lane, z planes per wave, float4 segments per lane per row}. */
 int sq_phi4_tile(sq_ctx *ctx, int out[4]);
+/* PHI4 slab decompositions: the ghost-zone depth G in use (= steps per halo
+ * exchange; multi-rank RCCL contexts pick it by timed trial blocks during the
+ * first sq_step / sq_run_frame calls) and the depth allocated; 0, 0 for a
+ * single periodic slab. */
+int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
 /* PHI4 observables over this process' slab: out[0] = sum phi, out[1] = sum
  * phi^2, out[2] = max |phi| (double accumulation on device). */
 int sq_moments(sq_ctx *ctx, double out[3]);

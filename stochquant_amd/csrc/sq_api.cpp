@@ -116,7 +116,10 @@ struct sq_ctx {
     long long Lz = 0;
     sq::Phi4Geom geom{};
     int zc = 8;
-    int gz = 1;  // ghost-zone depth (planes) of slab decompositions = steps per halo exchange
+    int gz = 1;    // active ghost-zone depth (planes) of slab decompositions = steps per halo exchange
+    int gpad = 1;  // allocated ghost planes on either side of each slab (gz <= gpad)
+    bool g_auto = false, g_tuned = false;  // ghost depth chosen by timed trial blocks (phi4_autotune)
+    double *dtune = nullptr;
     std::vector<Slab> slabs;
     int cur = 0;
     int *flag = nullptr;
@@ -183,8 +186,8 @@ int ev_begin(sq_ctx *c, hipStream_t s, EvPair **out) {
 
 size_t plane_floats(const sq_ctx *c) { return (size_t)c->Lx * (size_t)c->Ly; }
 
-// Local plane 0 of buffer k (the ghost zone is the c->gz planes on either side).
-float *plane0(const sq_ctx *c, const Slab &s, int k) { return s.buf[k] + (size_t)c->gz * plane_floats(c); }
+// Local plane 0 of buffer k (the ghost zone is the c->gpad planes on either side).
+float *plane0(const sq_ctx *c, const Slab &s, int k) { return s.buf[k] + (size_t)c->gpad * plane_floats(c); }
 
 sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     sq::Phi4StepArgs a{};
@@ -193,7 +196,7 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.Lx = c->Lx;
     a.Ly = c->Ly;
     a.nz = s.nz;
-    a.gz = c->gz;
+    a.gz = c->gpad;
     a.zg0 = s.z0;
     a.Lzg = c->Lz;
     const float h = (float)c->dtau;
@@ -290,7 +293,7 @@ int phi4_block(sq_ctx *c, int g) {
             SQ_HIP(hipMemcpyAsync(plane0(c, dn, cur) + (size_t)dn.nz * plane, p0, gbytes,
                                   hipMemcpyDeviceToDevice, s.sB));
             // my top G planes -> upper neighbour's lower ghosts [-G, 0)
-            SQ_HIP(hipMemcpyAsync(up.buf[cur], p0 + (size_t)(s.nz - G) * plane, gbytes,
+            SQ_HIP(hipMemcpyAsync(plane0(c, up, cur) - (size_t)G * plane, p0 + (size_t)(s.nz - G) * plane, gbytes,
                                   hipMemcpyDeviceToDevice, s.sB));
             SQ_HIP(hipEventRecord(s.evC, s.sB));
             c->perf.halo_bytes += 2.0 * (double)gbytes;
@@ -304,7 +307,7 @@ int phi4_block(sq_ctx *c, int g) {
         SQ_NCCL(ncclGroupStart());
         SQ_NCCL(ncclSend(p0 + (size_t)(s.nz - G) * plane, n, ncclFloat32, up, c->comm, s.sB));
         SQ_NCCL(ncclSend(p0, n, ncclFloat32, dn, c->comm, s.sB));
-        SQ_NCCL(ncclRecv(s.buf[cur], n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCL(ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, s.sB));
         SQ_NCCL(ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
         SQ_NCCL(ncclGroupEnd());
         SQ_HIP(hipEventRecord(s.evC, s.sB));
@@ -362,6 +365,58 @@ int phi4_block(sq_ctx *c, int g) {
     return SQ_OK;
 }
 
+// Ghost depth by measurement (slab paths): G in {4, 8, 16} (<= the allocated
+// depth), each timed over two blocks after one warm-up block on the interior
+// stream; across ranks the per-candidate times are max-reduced over RCCL so
+// every rank picks the same G (exchange sizes must match).  The trial steps
+// are ordinary steps: the field is the same for any G.
+int phi4_autotune(sq_ctx *c, int &n) {
+    std::vector<int> cand;
+    for (int g : {4, 8, 16})
+        if (g <= c->gpad) cand.push_back(g);
+    if (cand.empty()) cand.push_back(c->gpad);
+    int need = 0;
+    for (int g : cand) need += 3 * g;
+    if (n < need) return SQ_OK;  // too few steps requested: try again on a later call
+    hipEvent_t t0, t1;
+    SQ_HIP(hipEventCreate(&t0));
+    SQ_HIP(hipEventCreate(&t1));
+    std::vector<double> ms(cand.size());
+    for (size_t k = 0; k < cand.size(); ++k) {
+        const int g = cand[k];
+        c->gz = g;
+        int rc = phi4_block(c, g);
+        if (!rc) rc = phi4_join(c);
+        if (rc) return rc;
+        SQ_HIP(hipEventRecord(t0, c->slabs[0].sA));
+        for (int b = 0; b < 2 && !rc; ++b) rc = phi4_block(c, g);
+        if (rc) return rc;
+        SQ_HIP(hipEventRecord(t1, c->slabs[0].sA));
+        SQ_HIP(hipEventSynchronize(t1));
+        rc = phi4_join(c);
+        if (rc) return rc;
+        float e = 0;
+        SQ_HIP(hipEventElapsedTime(&e, t0, t1));
+        ms[k] = (double)e / (2.0 * g);
+        n -= 3 * g;
+    }
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (c->p.comm == SQ_COMM_RCCL && c->comm != nullptr) {
+        hipStream_t st = c->slabs[0].sA;
+        SQ_HIP(hipMemcpyAsync(c->dtune, ms.data(), sizeof(double) * ms.size(), hipMemcpyHostToDevice, st));
+        SQ_NCCL(ncclAllReduce(c->dtune, c->dtune, ms.size(), ncclFloat64, ncclMax, c->comm, st));
+        SQ_HIP(hipMemcpyAsync(ms.data(), c->dtune, sizeof(double) * ms.size(), hipMemcpyDeviceToHost, st));
+        SQ_HIP(hipStreamSynchronize(st));
+    }
+    size_t best = 0;
+    for (size_t k = 1; k < cand.size(); ++k)
+        if (ms[k] < ms[best]) best = k;
+    c->gz = cand[best];
+    c->g_tuned = true;
+    return SQ_OK;
+}
+
 int phi4_steps(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
         for (int i = 0; i < n; ++i) {
@@ -369,6 +424,10 @@ int phi4_steps(sq_ctx *c, int n) {
             if (rc) return rc;
         }
         return SQ_OK;
+    }
+    if (c->g_auto && !c->g_tuned) {
+        int rc = phi4_autotune(c, n);
+        if (rc) return rc;
     }
     while (n > 0) {
         const int g = std::min(n, c->gz);
@@ -445,8 +504,20 @@ int create_phi4(sq_ctx *c) {
         // ~28 us per exchange amortised over G steps against (G-1)/nz of
         // redundant ghost-zone planes.  G = nz/16 keeps the redundancy <= ~6 %.
         int g = (int)std::min(16ll, std::max(1ll, nz_min / 16));
-        if (const char *e = getenv("SQ_GHOST")) g = std::max(1, atoi(e));
+        // multi-rank RCCL runs measure G in {4, 8, 16} on the real link (the
+        // fixed cost and bandwidth of an xGMI exchange are not those of the
+        // one-GPU self-exchange these defaults were measured on); SQ_GHOST
+        // pins G, SQ_GHOST_AUTO=1 forces the trials on any slab path
+        c->g_auto = p.comm == SQ_COMM_RCCL && p.nranks > 1 && nz_min >= 64;
+        if (const char *e = getenv("SQ_GHOST_AUTO")) c->g_auto = atoi(e) != 0;
+        if (c->g_auto) g = (int)std::min(16ll, nz_min / 2);
+        if (const char *e = getenv("SQ_GHOST")) {
+            g = std::max(1, atoi(e));
+            c->g_auto = false;
+        }
         c->gz = (int)std::max(1ll, std::min((long long)g, nz_min));
+        c->gpad = c->gz;
+        SQ_HIP(hipMalloc(&c->dtune, 8 * sizeof(double)));
     }
     const size_t plane = plane_floats(c);
     for (int i = 0; i < nslab; ++i) {
@@ -454,7 +525,7 @@ int create_phi4(sq_ctx *c) {
         s.z0 = zs[i];
         s.nz = (int)(zs[i + 1] - zs[i]);
         if (s.nz < 1) return fail(SQ_E_ARG, "empty slab");
-        const size_t bytes = (size_t)(s.nz + 2 * c->gz) * plane * sizeof(float);
+        const size_t bytes = (size_t)(s.nz + 2 * c->gpad) * plane * sizeof(float);
         for (int k = 0; k < 2; ++k) {
             SQ_HIP(hipMalloc(&s.buf[k], bytes));
             SQ_HIP(hipMemset(s.buf[k], 0, bytes));
@@ -828,6 +899,7 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->g_st);
     (void)hipFree(c->flag);
     (void)hipFree(c->dacc);
+    (void)hipFree(c->dtune);
     (void)hipFree(c->dmax);
     if (c->qstream) (void)hipStreamDestroy(c->qstream);
     for (auto &e : c->evpool) {
@@ -991,6 +1063,14 @@ int sq_phi4_tile(sq_ctx *c, int out[4]) {
     out[1] = c->geom.r;
     out[2] = c->zc;
     out[3] = c->geom.v;
+    return SQ_OK;
+}
+
+int sq_phi4_ghost(sq_ctx *c, int *active, int *allocated) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (active) *active = c->p.comm == SQ_COMM_NONE ? 0 : c->gz;
+    if (allocated) *allocated = c->p.comm == SQ_COMM_NONE ? 0 : c->gpad;
     return SQ_OK;
 }
 

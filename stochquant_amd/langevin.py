@@ -252,6 +252,13 @@ class Phi4Lattice(_Ctx):
         _lib.call("sq_phi4_tile", self._h, out)
         return tuple(out)
 
+    @property
+    def ghost(self):
+        """(active, allocated) ghost-zone depth of a slab decomposition; (0, 0) for one periodic slab."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        _lib.call("sq_phi4_ghost", self._h, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
     def save(self, path):
         """Binary checkpoint: <path> (.npy float32 (nz, Ly, Lx)) + <path>.json (step, dtau, seed, z0)."""
         _lib.call("sq_save_field", self._h, os.fsencode(path))

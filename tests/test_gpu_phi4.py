@@ -315,3 +315,27 @@ def test_slice_correlator_across_slabs(gpu, oracle_mod):
         L.upload(phi0)
         L.step(3)
         assert np.array_equal(L.correlator(24), mono)
+
+
+@pytest.mark.parametrize("comm", ["loopback", "rccl"])
+def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
+    """Timed trial blocks pick G in {4, 8, 16}; the trial steps are ordinary
+    steps, so the field after them equals the single-slab run bit for bit."""
+    from stochquant_amd import unique_id
+    monkeypatch.setenv("SQ_GHOST_AUTO", "1")
+    shape = (256, 8, 128)
+    phi0 = _init(oracle_mod, shape)
+    steps = 100            # >= 3*(4+8+16) = 84 trial steps, then 16 more
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(steps)
+        mono = L.download()
+    kw = dict(comm="loopback", nslabs=2) if comm == "loopback" else \
+        dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id())
+    with _lat(shape, **kw) as L:
+        L.upload(phi0)
+        L.step(steps)
+        act, alloc = L.ghost
+        assert alloc == 16 and act in (4, 8, 16)
+        assert L.step_counter == steps
+        assert np.array_equal(L.download(), mono)
