@@ -365,6 +365,8 @@ int phi4_block(sq_ctx *c, int g) {
     return SQ_OK;
 }
 
+int phi4_join(sq_ctx *c);
+
 // Ghost depth by measurement (slab paths): G in {4, 8, 16} (<= the allocated
 // depth), each timed over two blocks after one warm-up block on the interior
 // stream; across ranks the per-candidate times are max-reduced over RCCL so
