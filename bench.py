@@ -187,6 +187,7 @@ def main():
                 "lattice": list(shape),
                 "per_gpu": [L, L, L],
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
+                "ghost_depth": lat.ghost[0] if slab_path else None,
                 "parallelism": "single GPU, one stream" if not slab_path else
                                f"z-slab x{world} ({a.comm if world == 1 else 'rccl'}), halo + boundary planes on "
                                f"stream B, interior on stream A",
