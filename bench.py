@@ -122,6 +122,8 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if slab_path:
+        lat.step(84)   # setup: the ghost-depth trial blocks (3 x (4 + 8 + 16) steps) when autotuning
     lat.step(a.warmup)
     lat.sync()
     torch.cuda.synchronize()
