@@ -42,6 +42,9 @@ def parse():
                     help="auto: one slab at N=1, RCCL slabs at N>1; rccl/loopback force the slab path "
                          "at N=1 (RCCL self-exchange / --slabs slabs on one GPU) to exercise it")
     ap.add_argument("--slabs", type=int, default=2)
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (config C5): the --size^3 lattice is split over the N GPUs "
+                         "instead of --size^3 per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU sample")
     ap.add_argument("--no-profile-events", action="store_true",
@@ -103,7 +106,7 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
     L = a.size
-    shape = (L, L, L * world)
+    shape = (L, L, L) if a.strong else (L, L, L * world)
     kw = dict(dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local)
     if world > 1:
         obj = [unique_id() if rank == 0 else None]
@@ -149,7 +152,7 @@ def main():
     # sanity: the field stayed finite and bounded (no guard hits)
     m = lat.moments()
     sites_local = lat.nz_local * L * L
-    total_updates = float(L ** 3) * world * a.steps
+    total_updates = float(shape[0] * shape[1] * shape[2]) * a.steps
     value = total_updates / t
     if perf["step_kernel_launches"] > 0:
         # region mean per step on the (interior) step-kernel stream; with slabs it
@@ -179,15 +182,16 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": t * 1e3 / a.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if a.strong else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": "synthetic (phi0 = 0.1*Philox normal, seed 0x5EED)",
             "config": {
                 "workload": f"phi^4 3-D Langevin step, {L}^3 fp32 per GPU (BASELINE configs[1]"
-                            f"{'' if world == 1 else ', weak-scaled slabs = configs[3]'})",
+                            f"{'' if world == 1 else ', weak-scaled slabs = configs[3]'})" if not a.strong else
+                            f"phi^4 3-D Langevin step, {L}^3 fp32 split over {world} GPU(s) (BASELINE configs[4], strong)",
                 "lattice": list(shape),
-                "per_gpu": [L, L, L],
+                "per_gpu": [L, L, lat.nz_local],
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
                 "ghost_depth": lat.ghost[0] if slab_path else None,
                 "parallelism": "single GPU, one stream" if not slab_path else
