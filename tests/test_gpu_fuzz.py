@@ -59,3 +59,27 @@ def test_serial_order_random_frames(gpu, oracle_mod, N, loops, ratio, a, seed):
     from test_gpu_qm1d_serial import _run_pair
     f0 = 0.3 * np.random.default_rng(seed).standard_normal(N)
     _run_pair(oracle_mod, N, a, ratio * a * a, 0, 1.0, loops, seed, 4, f0, check=_exact)
+
+
+@settings(max_examples=30, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(Lx=st.sampled_from([16, 64, 256, 512]), Ly=st.integers(1, 6), Lz=st.integers(2, 40),
+       nslabs=st.integers(2, 8), ghost=st.integers(1, 8), steps=st.integers(1, 20),
+       seed=st.integers(0, 2 ** 40))
+def test_slab_decomposition_random(gpu, oracle_mod, monkeypatch, Lx, Ly, Lz, nslabs, ghost, steps, seed):
+    """T5 as a property: any slab count and ghost depth gives
+    the monolithic field bit for bit, noise on."""
+    from stochquant_amd import Phi4Lattice
+    nslabs = min(nslabs, Lz)
+    shape = (Lx, Ly, Lz)
+    p = oracle_mod.phi4_params(shape, 0.02, 0.5, 1.0, seed)
+    phi = oracle_mod.phi4_init(p, 0.8)
+    with Phi4Lattice(shape, dtau=0.02, m2=0.5, lam=1.0, seed=seed) as L:
+        L.upload(phi)
+        L.step(steps)
+        mono = L.download()
+    monkeypatch.setenv("SQ_GHOST", str(ghost))
+    with Phi4Lattice(shape, dtau=0.02, m2=0.5, lam=1.0, seed=seed, comm="loopback", nslabs=nslabs) as L:
+        L.upload(phi)
+        L.step(steps)
+        assert np.array_equal(L.download(), mono)
