@@ -205,9 +205,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc_traffic(L, world),
-                "kernel": "phi4_step_kernel<QX=%d,R=%d,V=%d,MS=%s> zc=%d" % (
-                    lat.tile[0], lat.tile[1], lat.tile[3], str(L > 4 * lat.tile[0] * lat.tile[3]).lower(),
-                    lat.tile[2]),
+                "kernel": lat.kernel_name,
                 "timing": "hipEvent pair on the kernel stream around the timed launches (region mean)"
                           if perf["step_kernel_launches"] > 0 else "wall clock",
                 "algorithmic_bytes_per_launch": BYTES_PER_SITE * sites_per_launch,

@@ -136,6 +136,9 @@ int sq_slab(sq_ctx *ctx, long long *nz_local, long long *z0);
 /* PHI4 register tile of the step kernel: out = {lanes per x segment, rows
  * per lane, z planes per wave, float4 segments per lane per row}. */
 int sq_phi4_tile(sq_ctx *ctx, int out[4]);
+/* PHI4: the step kernel's template instance, as rocprofv3 names it, plus its
+ * z-chunk, e.g. "phi4_step_kernel<64, 1, 1, false, true, 3> zc=4". */
+int sq_phi4_kernel(sq_ctx *ctx, char *name, size_t cap);
 /* PHI4 slab decompositions: the ghost-zone depth G in use (= steps per halo
  * exchange; multi-rank RCCL contexts pick it by timed trial blocks during the
  * first sq_step / sq_run_frame calls) and the depth allocated; 0, 0 for a

@@ -95,6 +95,7 @@ SIGNATURES = {
     "sq_get_params": (ctypes.c_int, [_P, ctypes.POINTER(SqParams)]),
     "sq_save_field": (ctypes.c_int, [_P, ctypes.c_char_p]),
     "sq_load_field": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
+    "sq_phi4_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "sq_phi4_ghost": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "sq_qm1d_set_ordering": (ctypes.c_int, [_P, ctypes.c_int]),
     "sq_qm1d_set_lcg_seed": (ctypes.c_int, [_P, ctypes.c_ulonglong]),

@@ -1068,6 +1068,22 @@ int sq_phi4_tile(sq_ctx *c, int out[4]) {
     return SQ_OK;
 }
 
+int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
+    if (!c || !name || cap == 0) return fail(SQ_E_ARG, "bad argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    // the template arguments phi4_step_launch picks for the interior launch
+    // (rocprofv3 prints the kernel under exactly this name)
+    const bool ms = c->Lx / (4 * c->geom.qx * c->geom.v) > 1;
+    const bool nz = (float)(sqrt(2.0 * (double)(float)c->dtau) * c->p.C) != 0.0f;
+    int pf = c->geom.pf;
+    if (pf == 2 && !(c->geom.qx == 64 && c->geom.v == 1)) pf = 1;
+    if (pf >= 3 && c->geom.qx != 64) pf = 1;
+    if (pf == 5 && ms) pf = 3;
+    snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d> zc=%d", c->geom.qx, c->geom.r, c->geom.v,
+             ms ? "true" : "false", nz ? "true" : "false", pf, c->zc);
+    return SQ_OK;
+}
+
 int sq_phi4_ghost(sq_ctx *c, int *active, int *allocated) {
     if (!c) return fail(SQ_E_ARG, "null context");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");

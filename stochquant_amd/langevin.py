@@ -253,6 +253,13 @@ class Phi4Lattice(_Ctx):
         return tuple(out)
 
     @property
+    def kernel_name(self):
+        """The step kernel instance as rocprofv3 names it, plus the z-chunk."""
+        buf = ctypes.create_string_buffer(160)
+        _lib.call("sq_phi4_kernel", self._h, buf, len(buf))
+        return buf.value.decode()
+
+    @property
     def ghost(self):
         """(active, allocated) ghost-zone depth of a slab decomposition; (0, 0) for one periodic slab."""
         a, b = ctypes.c_int(), ctypes.c_int()
