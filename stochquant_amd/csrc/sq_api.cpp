@@ -523,7 +523,8 @@ int create_phi4(sq_ctx *c) {
     }
     const size_t plane = plane_floats(c);
     for (int i = 0; i < nslab; ++i) {
-        Slab s;
+        c->slabs.emplace_back();  // owned by the context from here on: sq_destroy frees a partial set-up
+        Slab &s = c->slabs.back();
         s.z0 = zs[i];
         s.nz = (int)(zs[i + 1] - zs[i]);
         if (s.nz < 1) return fail(SQ_E_ARG, "empty slab");
@@ -544,7 +545,6 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipEventRecord(s.evA, s.sA));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         SQ_HIP(hipEventRecord(s.evE, s.sA));
-        c->slabs.push_back(s);
     }
     SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
     SQ_HIP(hipMemset(c->flag, 0, sizeof(int)));
