@@ -336,11 +336,12 @@ int phi4_block(sq_ctx *c, int g) {
     }
     count_step(c);
     // 4. steps 1..g-1 on the shrinking extended range; the last one edges first
-    bool edges_recorded = false;
+    std::vector<char> edges_recorded(c->slabs.size(), 0);  // per slab: slabs of a decomposition differ in nz
     for (int st = 1; st < g; ++st) {
         const int in_buf = cur ^ (st & 1);
         const bool split = st == g - 1;
-        for (auto &s : c->slabs) {
+        for (size_t i = 0; i < c->slabs.size(); ++i) {
+            Slab &s = c->slabs[i];
             int rc;
             if (split && c->edge_first && s.nz > 2 * G) {
                 rc = phi4_launch_span(c, s, in_buf, s.sA, 0, G, true);
@@ -349,7 +350,7 @@ int phi4_block(sq_ctx *c, int g) {
                 if (rc) return rc;
                 SQ_HIP(hipEventRecord(s.evE, s.sA));
                 rc = phi4_launch_span(c, s, in_buf, s.sA, G, s.nz - G, false);
-                edges_recorded = true;
+                edges_recorded[i] = 1;
             } else {
                 rc = phi4_launch_span(c, s, in_buf, s.sA, -(g - 1 - st), s.nz + (g - 1 - st), true);
             }
@@ -357,9 +358,10 @@ int phi4_block(sq_ctx *c, int g) {
         }
         count_step(c);
     }
-    for (auto &s : c->slabs) {
+    for (size_t i = 0; i < c->slabs.size(); ++i) {
+        Slab &s = c->slabs[i];
         SQ_HIP(hipEventRecord(s.evA, s.sA));
-        if (!edges_recorded) SQ_HIP(hipEventRecord(s.evE, s.sA));
+        if (!edges_recorded[i]) SQ_HIP(hipEventRecord(s.evE, s.sA));
     }
     c->cur = cur ^ (g & 1);
     return SQ_OK;

@@ -339,3 +339,21 @@ def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
         assert alloc == 16 and act in (4, 8, 16)
         assert L.step_counter == steps
         assert np.array_equal(L.download(), mono)
+
+
+def test_uneven_slabs_edge_first(gpu, oracle_mod, monkeypatch):
+    """Slabs of different thickness in one decomposition: only the thicker ones
+    split their last step into edges + middle; each slab's exchange must wait on
+    its own edge event (regression: Lz = 31 over 5 slabs, G = 3)."""
+    shape = (16, 4, 31)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(10)
+        mono = L.download()
+    monkeypatch.setenv("SQ_GHOST", "3")
+    with _lat(shape, comm="loopback", nslabs=5) as L:
+        L.upload(phi0)
+        L.step(4)
+        L.step(6)
+        assert np.array_equal(L.download(), mono)
