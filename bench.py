@@ -35,7 +35,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=2000,
+                    help="untimed steps first (clocks settle: 2000 vs 200 measured +2.8 %%, profiles/r01/warmup_ab.log)")
     ap.add_argument("--size", type=int, default=256, help="per-GPU lattice edge (default 256 = config C2)")
     ap.add_argument("--dtau", type=float, default=0.01)
     ap.add_argument("--comm", choices=["auto", "rccl", "loopback"], default="auto",
