@@ -208,8 +208,9 @@ __global__ __launch_bounds__(256) void gs_xi_kernel(const uint32_t *w1, const ui
 // noise is loaded one chunk ahead (the next phase's first chunk while the
 // last chunk of this phase computes).
 template <int CH>
-__global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B) {
+__global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B, int om_lds) {
     extern __shared__ double s_f[];  // the field, updated in place (the serial order's f)
+    double *s_om = s_f + A.N;        // om_lds: omega of every step, read once per phase
     const int N = A.N, loops = A.loops, pot = A.pot;
     const int lane = threadIdx.x;
     const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
@@ -234,7 +235,10 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B)
                 else if (nw < 0) w = -nw;
                 else w = nw;
             }
-            if (lane < nb) A.om[jb + lane] = mine;
+            if (lane < nb) {
+                A.om[jb + lane] = mine;
+                if (om_lds) s_om[jb + lane] = mine;
+            }
         }
         if (lane == 0) A.om[loops] = w;
     }
@@ -242,7 +246,6 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B)
 
     double lastnew = 0., lastold = 0.;  // my block's last site after / before my current step
     const int nchunk = (B + CH - 1) / CH;
-    double cur[CH], nxt[CH];
     auto load_chunk = [&](double (&dst)[CH], int j, int c) {
 #pragma unroll
         for (int q = 0; q < CH; ++q) {
@@ -250,58 +253,97 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B)
             dst[q] = (owner && j >= 0 && j < loops && i < i1) ? A.xi[(size_t)j * (N + 1) + i] : 0.;
         }
     };
-    load_chunk(cur, -lane, 0);
-    const int nphase = nl - 1 + loops;
-    for (int p = 0; p < nphase; ++p) {
-        const int j = p - lane;
+    // state carried between the chunks of one phase
+    double prev_new = 0., prev_old = 0., firstval = 0., rfirst = 0.;
+    // sites c*CH .. c*CH+CH-1 of this lane's block at step j, noise in cur
+    auto run_chunk = [&](int j, int c, const double (&cur)[CH]) {
         const bool act = owner && j >= 0 && j < loops;
         const bool last = j == loops - 1;
-        const double w = act ? A.om[j] : 0.;
-        const double lnew = __shfl_up(lastnew, 1, 64);
-        const double lold = __shfl_up(lastold, 1, 64);
-        double prev_new = lnew, prev_old = lold, firstval = 0., rfirst = 0.;
-        for (int c = 0; c < nchunk; ++c) {
-            if (c + 1 < nchunk) load_chunk(nxt, j, c + 1);
-            else load_chunk(nxt, j + 1, 0);
+        const double w = act ? (om_lds ? s_om[j] : A.om[j]) : 0.;
+        // off the serial chain: old values, potential term, noise (same
+        // sub-expressions the chain below combines in the reference's order)
+        double fi[CH], rr[CH], t2[CH], dw[CH];
 #pragma unroll
-            for (int q = 0; q < CH; ++q) {
-                const int b = c * CH + q;
-                const int i = i0 + b;
-                const bool valid = act && i < i1;
-                if (b == B - 1) rfirst = __shfl_down(firstval, 1, 64);  // lane l+1's first site, its step j-1
-                if (b < B) {
-                    const double fi = i < N ? s_f[i] : 0.;
-                    double v = fi;
-                    if (valid) {
-                        const double L = last ? prev_old : prev_new;
-                        double s;
-                        if (i == 0) {
-                            const double R = N > 1 ? s_f[1] : 0.;  // N >= 2; i + 1 < i1 since B >= 2
-                            s = R + (-kEta) - xcl(-1. * a, w, pot) - 2 * fi;
-                        } else if (i == N - 1) {
-                            s = L + kEta - xcl((double)N * a, w, pot) - 2 * fi;
-                        } else {
-                            const double R = b == B - 1 ? rfirst : s_f[i + 1];
-                            s = R + L - 2 * fi;
-                        }
-                        v = fi + kM * h * s / a2 - ddpot(xcl((double)i * a, w, pot), pot) * fi * h + sig * cur[q];
-                        v = guard(v);
-                        A.hist[(size_t)j * N + i] = v;
-                        if (!last) s_f[i] = v;
-                    }
-                    prev_old = fi;
-                    prev_new = v;
-                    if (b == 0) firstval = v;  // = s_f[i0] after this phase's update (old value if idle)
-                    if (b == B - 1 || i == i1 - 1) {
-                        if (i == i1 - 1) {
-                            lastnew = v;
-                            lastold = fi;
-                        }
-                    }
+        for (int q = 0; q < CH; ++q) {
+            const int b = c * CH + q;
+            const int i = i0 + b;
+            fi[q] = (b < B && i < N) ? s_f[i] : 0.;
+            rr[q] = (b < B - 1 && i + 1 < N) ? s_f[i + 1] : 0.;  // right neighbour inside the block: old
+            t2[q] = ddpot(xcl((double)i * a, w, pot), pot) * fi[q] * h;
+            dw[q] = sig * cur[q];
+        }
+        const double xlo = xcl(-1. * a, w, pot), xhi = xcl((double)N * a, w, pot);
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const int b = c * CH + q;
+            const int i = i0 + b;
+            const bool valid = act && i < i1;
+            if (b == B - 1) rfirst = __shfl_down(firstval, 1, 64);  // lane l+1's first site, its step j-1
+            if (b < B) {
+                double v = fi[q];
+                if (valid) {
+                    const double L = last ? prev_old : prev_new;
+                    double sum;
+                    if (i == 0) sum = rr[q] + (-kEta) - xlo - 2 * fi[q];  // N >= 2, B >= 2: rr = f[1]
+                    else if (i == N - 1) sum = L + kEta - xhi - 2 * fi[q];
+                    else sum = (b == B - 1 ? rfirst : rr[q]) + L - 2 * fi[q];
+                    v = fi[q] + kM * h * sum / a2 - t2[q] + dw[q];
+                    v = guard(v);
+                    A.hist[(size_t)j * N + i] = v;
+                    if (!last) s_f[i] = v;
+                }
+                prev_old = fi[q];
+                prev_new = v;
+                if (b == 0) firstval = v;  // = s_f[i0] after this phase's update (old value if idle)
+                if (i == i1 - 1) {
+                    lastnew = v;
+                    lastold = fi[q];
                 }
             }
+        }
+    };
+    auto begin_phase = [&]() {
+        prev_new = __shfl_up(lastnew, 1, 64);  // lane l-1's last site, its step j (previous phase)
+        prev_old = __shfl_up(lastold, 1, 64);
+        firstval = rfirst = 0.;
+    };
+    const int nphase = nl - 1 + loops;
+    if (nchunk == 1) {
+        // one chunk per phase: a phase is short, so the noise is prefetched
+        // four phases ahead through a four-slot register ring
+        double r0[CH], r1[CH], r2[CH], r3[CH];
+        load_chunk(r0, 0 - lane, 0);
+        load_chunk(r1, 1 - lane, 0);
+        load_chunk(r2, 2 - lane, 0);
+        load_chunk(r3, 3 - lane, 0);
+        auto phase = [&](int p, double (&slot)[CH]) {
+            begin_phase();
+            run_chunk(p - lane, 0, slot);
+            load_chunk(slot, p + 4 - lane, 0);
+        };
+        for (int p = 0; p < nphase; p += 4) {
+            phase(p, r0);
+            if (p + 1 >= nphase) break;
+            phase(p + 1, r1);
+            if (p + 2 >= nphase) break;
+            phase(p + 2, r2);
+            if (p + 3 >= nphase) break;
+            phase(p + 3, r3);
+        }
+    } else {
+        // several chunks per phase: the next chunk is prefetched while this one computes
+        double cur[CH], nxt[CH];
+        load_chunk(cur, -lane, 0);
+        for (int p = 0; p < nphase; ++p) {
+            const int j = p - lane;
+            begin_phase();
+            for (int c = 0; c < nchunk; ++c) {
+                if (c + 1 < nchunk) load_chunk(nxt, j, c + 1);
+                else load_chunk(nxt, j + 1, 0);
+                run_chunk(j, c, cur);
 #pragma unroll
-            for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
+                for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
+            }
         }
     }
 }
@@ -353,20 +395,50 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
     int E = A.st->lrgEl;
     double V = A.st->lrgVl;
     int brk_step = -1, brk_item = -1;
+    double w_next = A.om[0];
+    // B <= KP sites per lane: the next step's history row and noise are loaded
+    // into registers while this step is scanned (the loads' latency is then
+    // off the per-step critical path)
+    constexpr int KP = 16;
+    double pr[KP], px[KP];
+    auto prefetch = [&](int j) {
+        const double *row = A.hist + (size_t)j * N;
+        const double *xr = A.xi + (size_t)j * (N + 1);
+#pragma unroll
+        for (int b = 0; b < KP; ++b) {
+            const int i = i0 + b;
+            pr[b] = i < i1 ? row[i] : 0.;
+            px[b] = i < i1 ? xr[i] : 0.;
+        }
+    };
+    if (B <= KP) prefetch(0);
     for (int j = 0; j < loops; ++j) {
-        const double w = A.om[j];
+        const double w = w_next;
+        if (j + 1 < loops) w_next = A.om[j + 1];  // in flight during this step
         const double *row = A.hist + (size_t)j * N;
         const double *xr = A.xi + (size_t)j * (N + 1);
         // nf[E] as the serial order sees it before item E runs this step:
         // the previous step's value (the persistent newf buffer at j = 0)
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
         const double T0 = nfE + xcl((double)E * a, w, pot);
-        // this step's global inputs, staged once (loads issued back to back)
+        // this step's global inputs, staged once
+        if (B <= KP) {
+#pragma unroll
+            for (int b = 0; b < KP; ++b) {
+                const int i = i0 + b;
+                if (i < i1) {
+                    s_n[i] = pr[b];
+                    s_d[i] = absol(pr[b] - s_f[i] - sig * px[b]);  // :139, |nf - f - dw|
+                }
+            }
+            if (j + 1 < loops) prefetch(j + 1);
+        } else {
 #pragma unroll 4
-        for (int i = i0; i < i1; ++i) {
-            const double v = row[i];
-            s_n[i] = v;
-            s_d[i] = absol(v - s_f[i] - sig * xr[i]);  // :139, |nf - f - dw|
+            for (int i = i0; i < i1; ++i) {
+                const double v = row[i];
+                s_n[i] = v;
+                s_d[i] = absol(v - s_f[i] - sig * xr[i]);  // :139, |nf - f - dw|
+            }
         }
         double m1 = NEG;
         for (int i = i0; i < min(i1, E); ++i) m1 = fmax(m1, s_n[i] + xcl((double)i * a, w, pot));
@@ -453,7 +525,213 @@ __global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
     }
 }
 
+// ------------------------------------------------- scan, register path ----
+// Wave-wide max-scans by DPP (row_shr 1/2/4/8, row_bcast 15/31: the gfx9
+// inclusive-scan sequence), no LDS round trips; 64-bit values move as two
+// 32-bit DPP halves.  Out-of-range lanes read the identity (bound_ctrl off).
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_d(double v, double id) {
+    const int lo = __builtin_amdgcn_update_dpp((int)__double2loint(id), (int)__double2loint(v), CTRL, RM, BM, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)__double2hiint(id), (int)__double2hiint(v), CTRL, RM, BM, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_i(int v, int id) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, RM, BM, false);
+}
+__device__ __forceinline__ double dpp_incl_max(double v) {
+    const double id = -__builtin_inf();
+    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x114, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x118, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v, id));
+    return v;
+}
+__device__ __forceinline__ double dpp_excl_max(double v) {  // max over lanes < this lane
+    return dpp_d<0x138, 0xf, 0xf>(dpp_incl_max(v), -__builtin_inf());  // wave_shr:1
+}
+__device__ __forceinline__ double dpp_all_max(double v) {
+    const double s = dpp_incl_max(v);
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(s), 63),
+                            __builtin_amdgcn_readlane(__double2loint(s), 63));
+}
+__device__ __forceinline__ int dpp_all_max_i(int v) {
+    const int id = (int)0x80000000;
+    v = max(v, dpp_i<0x111, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x112, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x114, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x118, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x142, 0xa, 0xf>(v, id));
+    v = max(v, dpp_i<0x143, 0xc, 0xf>(v, id));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
+
+// N <= 64 KB: the lane's KB sites stay in registers (field, running means,
+// this step's X, |X|, drift check), the next step's inputs are prefetched, and
+// only f / nf go through LDS for the cross-lane reads of nf[E] and f[mid].
+// Same semantics and expression order as gs_scan_kernel.
+template <int KB>
+__global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
+    extern __shared__ double lds[];
+    const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
+    double *s_f = lds, *s_n = lds + N;
+    const int lane = threadIdx.x;
+    const int B = (N + 63) / 64;
+    const int i0 = lane * B, i1 = min(N, i0 + B);
+    const double a = A.a, sig = A.sig;
+    const double NEG = -__builtin_inf();
+    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB];
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+        const int i = i0 + b;
+        const bool in = b < B && i < i1;
+        f_[b] = in ? A.f0[i] : 0.;
+        x_[b] = in ? A.x0[i] : 0.;
+        xx_[b] = in ? A.xx00[i] : 0.;
+        if (in) s_f[i] = f_[b];
+    }
+    auto prefetch = [&](int j) {
+        const double *row = A.hist + (size_t)j * N;
+        const double *xr = A.xi + (size_t)j * (N + 1);
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            const bool in = b < B && i < i1;
+            pr[b] = in ? row[i] : 0.;
+            px[b] = in ? xr[i] : 0.;
+        }
+    };
+    prefetch(0);
+    __syncthreads();
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int brk_step = -1, brk_item = -1;
+    double w_next = A.om[0];
+    double n[KB];
+    for (int j = 0; j < loops; ++j) {
+        const double w = w_next;
+        if (j + 1 < loops) w_next = A.om[j + 1];
+        double X[KB], D[KB], xc[KB];
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            n[b] = pr[b];
+            xc[b] = xcl((double)i * a, w, pot);
+            X[b] = n[b] + xc[b];
+            D[b] = absol(n[b] - f_[b] - sig * px[b]);  // :139, |nf - f - dw|
+            if (b < B && i < i1) s_n[i] = n[b];
+        }
+        if (j + 1 < loops) prefetch(j + 1);
+        // nf[E] before item E runs this step: the previous step's value
+        // (the persistent newf buffer at j = 0)
+        const double nfE = j == 0 ? A.nfp[E] : s_f[E];
+        const double T0 = nfE + xcl((double)E * a, w, pot);
+        double m1 = NEG, ty = NEG, ta = NEG;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            if (b < B && i < i1) {
+                if (i < E) m1 = fmax(m1, X[b]);
+                ta = fmax(ta, absol(X[b]));
+            }
+        }
+        const bool caseB = dpp_all_max(m1) > T0;  // a leader before E: no reset at item E
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            if (b < B && i < i1 && (caseB || i >= E)) ty = fmax(ty, X[b]);
+        }
+        double py = dpp_excl_max(ty), pa = dpp_excl_max(ta);
+        const double base = caseB ? T0 : NEG;
+        int first_bad = 0x7fffffff, last_lead = -1;
+        double Vbad = 0.;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            if (b < B && i < i1) {
+                const double th = fmax(base, py);
+                const bool lead = (caseB || i > E) && X[b] > th;
+                const double Vi = fmax(V, pa);  // V seen by item i (max over k < i)
+                if (lead) {
+                    last_lead = i;
+                    if (D[b] > Vi && i < first_bad) {
+                        first_bad = i;
+                        Vbad = fmax(Vi, absol(X[b]));
+                    }
+                }
+                if (caseB || i >= E) py = fmax(py, X[b]);
+                pa = fmax(pa, absol(X[b]));
+            }
+        }
+        const int kb = dpp_all_min_i(first_bad);
+        if (kb != 0x7fffffff && j > 0) {  // items after kb see stable != 1 and never run this round
+            E = kb;
+            V = __shfl(Vbad, kb / B, 64);
+            brk_step = j;
+            brk_item = kb;
+            break;
+        }
+        const int ll = dpp_all_max_i(last_lead);
+        if (ll >= 0) E = ll;
+        V = fmax(V, dpp_all_max(ta));
+        if (kb != 0x7fffffff) {  // round 0: the stable test only starts at round 1 (:168-171)
+            brk_step = 0;
+            brk_item = N;
+            break;
+        }
+        __syncthreads();  // s_n of every lane written (f[mid] new)
+        const double den = (double)(A.runs + j + 1);
+        const double xm = xcl((double)mid * a, w, pot);
+        const double fm_old = s_f[mid], fm_new = s_n[mid];
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            const double g = f_[b] + xc[b];
+            const double fm = (i > mid && j < loops - 1) ? fm_new : fm_old;
+            xx_[b] = xx_[b] + (g * (fm + xm) - xx_[b]) / den;
+            x_[b] = x_[b] + (g - x_[b]) / den;
+        }
+        __syncthreads();  // every lane has read s_f[mid] before it is overwritten
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            f_[b] = n[b];
+            if (b < B && i < i1) s_f[i] = n[b];
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+        const int i = i0 + b;
+        if (!(b < B && i < i1)) continue;
+        if (brk_step < 0) {
+            A.nf[i] = f_[b];
+            A.nfp[i] = f_[b];
+            A.nx[i] = x_[b];
+            A.nxx0[i] = xx_[b];
+        } else if (i <= brk_item) {
+            A.nfp[i] = n[b];
+        } else if (brk_step > 0) {
+            A.nfp[i] = f_[b];  // still the previous round's value
+        }
+    }
+    if (lane == 0) {
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = brk_step < 0 ? 1 : 0;
+        A.st->steps_done = brk_step < 0 ? loops : brk_step + 1;
+        A.st->omega_out = A.om[loops];
+        A.st->consumed = brk_step < 0 ? (long long)loops * (N + 1)
+                                      : (long long)brk_step * (N + 1) + brk_item + 1;
+    }
+}
+
 }  // namespace
+
+constexpr int kSweepLdsMax = 96 * 1024;
 
 int qm1d_gs_block(int N) {
     if (N < 2 || N > kQm1dGsMaxN) return 0;
@@ -483,14 +761,24 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
                                      (int)(5 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
             return e;
         for (const void *k : {(const void *)gs_sweep_kernel<2>, (const void *)gs_sweep_kernel<8>})
-            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kSweepLdsMax)) != hipSuccess)
                 return e;
         attr = true;
     }
-    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(64), lds1, s, a, B);
-    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(64), lds1, s, a, B);
-    hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds5, s, a);
+    // omega of all steps next to the field in LDS when it fits (one LDS read per phase
+    // instead of a global load on the pipeline's critical path)
+    const size_t lds_om = sizeof(double) * ((size_t)a.N + a.loops + 1);
+    const int om_lds = lds_om <= (size_t)kSweepLdsMax ? 1 : 0;
+    const size_t lds_sw = om_lds ? lds_om : lds1;
+    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(64), lds_sw, s, a, B, om_lds);
+    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(64), lds_sw, s, a, B, om_lds);
+    const int B3 = (a.N + 63) / 64;
+    const size_t lds2 = 2 * lds1;
+    if (B3 <= 2) hipLaunchKernelGGL(gs_scan_reg_kernel<2>, dim3(1), dim3(64), lds2, s, a);
+    else if (B3 <= 4) hipLaunchKernelGGL(gs_scan_reg_kernel<4>, dim3(1), dim3(64), lds2, s, a);
+    else if (B3 <= 8) hipLaunchKernelGGL(gs_scan_reg_kernel<8>, dim3(1), dim3(64), lds2, s, a);
+    else if (B3 <= 16) hipLaunchKernelGGL(gs_scan_reg_kernel<16>, dim3(1), dim3(64), lds2, s, a);
+    else hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds5, s, a);
     return hipGetLastError();
 }
 
