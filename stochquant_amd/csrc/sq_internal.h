@@ -20,7 +20,7 @@ int set_error(int code, const std::string &msg);
 struct Phi4StepArgs {
     const float *in;
     float *out;
-    int Lx, Ly, nz, gz;
+    int Lx, Ly, nz, gz;            // gz: ghost planes allocated on either side (local plane 0 is padded plane gz)
     int zlo, zhi, zstep, zc, nzc;  // chunk k updates planes [zlo + k*zstep, +zc) clipped to zhi
     int periodic;
     int nxseg, nyg, nunits;
