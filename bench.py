@@ -104,6 +104,8 @@ def main():
     _lib.load()  # fail loudly if the HIP library is missing
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
     L = a.size
