@@ -19,6 +19,7 @@
 // SQ_ORDER=serial selects the reference's own serial order instead
 // (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
 // SQ_ORDER_SERIAL in stochquant.h), N <= 3072.
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -29,6 +30,8 @@
 #include "../../include/stochquant.h"
 
 namespace {
+
+std::chrono::steady_clock::time_point t_start;
 
 double absol(double v) { return v <= 0 ? -v : v; }
 
@@ -76,6 +79,25 @@ int die(const char *what, sq_ctx *ctx) {
     fprintf(stderr, "tauhost: %s: %s\n", what, sq_last_error());
     if (ctx) sq_destroy(ctx);
     return 1;
+}
+
+// SQ_PERF_JSON=<path>: one JSON perf record per run (SURVEY.md §5 "Metrics"):
+// steps, site updates, time inside the frames, the rate, final Δτ.
+void write_perf(sq_ctx *ctx, const char *model, int frames, double wall_s) {
+    const char *path = getenv("SQ_PERF_JSON");
+    if (!path) return;
+    sq_perf_t pf;
+    double dt = 0;
+    if (sq_perf(ctx, &pf) != SQ_OK || sq_get_dtau(ctx, &dt) != SQ_OK) return;
+    FILE *fp = fopen(path, "w");
+    if (!fp) return;
+    const double s = pf.frame_ms * 1e-3;
+    fprintf(fp,
+            "{\"model\": \"%s\", \"frames\": %d, \"steps\": %lld, \"site_updates\": %lld, "
+            "\"frame_seconds\": %.6f, \"wall_seconds\": %.6f, \"site_updates_per_s\": %.6g, "
+            "\"deltatau_final\": %.17g}\n",
+            model, frames, pf.steps, pf.site_updates, s, wall_s, s > 0 ? (double)pf.site_updates / s : 0.0, dt);
+    fclose(fp);
 }
 
 double env_double(const char *name, double dflt) {
@@ -164,6 +186,8 @@ int run_phi4(int N, double deltatau, int frames, double C, int dev, int fps, int
         sq_destroy(ctx);
         return 1;
     }
+    write_perf(ctx, "phi4", frames,
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
     sq_destroy(ctx);
     return 0;
 }
@@ -171,6 +195,7 @@ int run_phi4(int N, double deltatau, int frames, double C, int dev, int fps, int
 }  // namespace
 
 int main(int argc, char **argv) {
+    t_start = std::chrono::steady_clock::now();
     if (argc < 14) {
         fprintf(stderr,
                 "usage: %s N deltat deltatau frames potID C dev fps inTime loops startFile|0 "
@@ -310,6 +335,8 @@ int main(int argc, char **argv) {
         fprintf(fp, "% -*e|deltaTau\n", endAccuracy, dtautmp);
         fclose(fp);
     }
+    write_perf(ctx, "qm1d", frames,
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
     sq_destroy(ctx);
     return 0;
 }

@@ -164,7 +164,10 @@ def test_phi4_mode_through_the_cli(gpu, tmp_path):
     from stochquant_amd import Phi4Lattice, parse_frame_line
     env = dict(SQ_MODEL="phi4", SQ_SHAPE="64x16x32", SQ_SEED="7", SQ_M2="0.5", SQ_LAMBDA="1.5")
     argv = lambda frames, start: ["32", "1", "0.01", str(frames), "0", "1", "0", "1", "0", "10", start, "END", "12"]
-    out, _ = _run_env(tmp_path, argv(4, "0"), **env)
+    out, _ = _run_env(tmp_path, argv(4, "0"), SQ_PERF_JSON=str(tmp_path / "perf.json"), **env)
+    import json
+    perf = json.loads((tmp_path / "perf.json").read_text())
+    assert perf["model"] == "phi4" and perf["steps"] == 40 and perf["site_updates"] == 40 * 64 * 16 * 32
     lines = out.strip().split("\n")
     assert len(lines) == 4
     for k, ln in enumerate(lines):
