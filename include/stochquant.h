@@ -105,7 +105,7 @@ int sq_qm1d_set_scan(sq_ctx *ctx, int lrgEl, double lrgVl, unsigned long long ti
  * serial semantics of time_dev: Gauss-Seidel order,
  * the last step of a frame Jacobi, the racy stability scan as the in-order
  * scan, the break after the first unstable item, newf / lrgEl / lrgVl / the
- * seed never rolled back.  2 <= N <= 3072.  Its noise is the reference's
+ * seed never rolled back.  2 <= N <= 4096.  Its noise is the reference's
  * random() (tau_kernel.cl:269-284) on the shared seed rand1 (tauhost.c:185):
  * sq_qm1d_set_lcg_seed sets it, each frame advances it by the calls it made
  * (sq_qm1d_noise_consumed).  sq_qm1d_inject_noise replaces the next frame's

@@ -105,7 +105,7 @@ struct Qm1dGsArgs {
     double a, a2, h, sig, sigw, kconst;
 };
 
-constexpr int kQm1dGsMaxN = 3072;  // the scan kernel keeps 5N doubles in LDS (120 KiB)
+constexpr int kQm1dGsMaxN = 4096;  // <= 4 sites per thread of a 1024-thread block; 2N doubles of LDS
 int qm1d_gs_block(int N);  // sites per lane of the sweep pipeline, 0 if N unsupported
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
                               uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s);

@@ -16,15 +16,16 @@
 //                    log/cos via fp64; glibc's logf/cosf round differently in
 //                    ~1% of arguments, so xi is within 1 ulp of the oracle's,
 //                    and bit-exact when the stream is injected).
-//   gs_sweep_kernel  one wave: the GS field sweep as a skewed pipeline.  Lane l
-//                    owns sites [lB, lB+B) and runs step j in phase p = l + j:
-//                    the left neighbour's step-j value comes from lane l-1's
-//                    previous phase, the right neighbour's step-(j-1) value
-//                    from lane l+1's first site of the same phase.  Every
+//   gs_sweep_kernel  one block (<= 16 waves): the GS field sweep as a skewed
+//                    pipeline.  Thread l owns sites [lB, lB+B) and runs step j
+//                    in phase p = l + j: the left neighbour's step-j value comes
+//                    from thread l-1's previous phase, the right neighbour's
+//                    step-(j-1) value from thread l+1's first site of the same
+//                    phase (lane shuffles inside a wave, LDS across waves).  Every
 //                    (step, site) is computed exactly as the serial order
 //                    computes it, with the reference's expression order.  The
 //                    field of every step goes to hist (loops x N).
-//   gs_scan_kernel   one wave: walks the steps in order and evaluates the
+//   gs_scan_*_kernel one block: walks the steps in order and evaluates the
 //                    stability scan (tau_kernel.cl:135-143) as prefix maxima
 //                    (derivation in DESIGN.md §QM1D serial mode), finds the
 //                    first unstable item (the serial break: items after it
@@ -204,22 +205,27 @@ __global__ __launch_bounds__(256) void gs_xi_kernel(const uint32_t *w1, const ui
 }
 
 // -------------------------------------------------------------- sweep ----
-// Lane l's step j happens in phase l + j.  CH sites per chunk; the chunk's
-// noise is loaded one chunk ahead (the next phase's first chunk while the
-// last chunk of this phase computes).
+// Pipeline lane g (= thread index; W = blockDim/64 waves) runs step j in
+// phase g + j.  Inside a wave the neighbour values move by lane shuffles; the
+// two wave-edge values of a phase go through LDS, with one barrier after the
+// first site of the phase (right neighbour's step-(j-1) value) and one at its
+// end (left neighbour's step-j value).  CH sites per chunk; the noise of a
+// single-chunk phase is prefetched four phases ahead, of a multi-chunk phase
+// one chunk ahead.
 template <int CH>
-__global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B, int om_lds) {
+__global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int B, int om_lds) {
     extern __shared__ double s_f[];  // the field, updated in place (the serial order's f)
     double *s_om = s_f + A.N;        // om_lds: omega of every step, read once per phase
+    __shared__ double s_enew[16], s_eold[16], s_efirst[16];  // wave edges of the current phase
     const int N = A.N, loops = A.loops, pot = A.pot;
-    const int lane = threadIdx.x;
+    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
     const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
     const int nl = (N + B - 1) / B;
-    const int i0 = lane * B, i1 = min(N, i0 + B);
-    const bool owner = lane < nl;
+    const int i0 = g * B, i1 = min(N, i0 + B);
+    const bool owner = g < nl;
 
-    for (int i = lane; i < N; i += 64) s_f[i] = A.f0[i];
-    {  // omega of every step: item N's update, :103-110,155-167.  64 draws
+    for (int i = g; i < N; i += blockDim.x) s_f[i] = A.f0[i];
+    if (wv == 0) {  // omega of every step: item N's update, :103-110,155-167.  64 draws
        // per batch land in lanes; the (wave-uniform) recurrence reads them
        // with readlane, and lane q keeps omega of step jb + q.
         double w = A.st->omega_in;
@@ -278,7 +284,10 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B,
             const int b = c * CH + q;
             const int i = i0 + b;
             const bool valid = act && i < i1;
-            if (b == B - 1) rfirst = __shfl_down(firstval, 1, 64);  // lane l+1's first site, its step j-1
+            if (b == B - 1) {  // lane g+1's first site, its step j-1 (computed at b = 0 of this phase)
+                rfirst = __shfl_down(firstval, 1, 64);
+                if (W > 1 && lane == 63 && wv < W - 1) rfirst = s_efirst[wv + 1];
+            }
             if (b < B) {
                 double v = fi[q];
                 if (valid) {
@@ -300,26 +309,44 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B,
                     lastold = fi[q];
                 }
             }
+            if (W > 1 && b == 0) {  // publish the wave's first value for the wave below
+                if (lane == 0) s_efirst[wv] = firstval;
+                __syncthreads();
+            }
         }
     };
     auto begin_phase = [&]() {
-        prev_new = __shfl_up(lastnew, 1, 64);  // lane l-1's last site, its step j (previous phase)
+        prev_new = __shfl_up(lastnew, 1, 64);  // lane g-1's last site, its step j (previous phase)
         prev_old = __shfl_up(lastold, 1, 64);
+        if (W > 1 && lane == 0 && wv > 0) {
+            prev_new = s_enew[wv - 1];
+            prev_old = s_eold[wv - 1];
+        }
         firstval = rfirst = 0.;
+    };
+    auto end_phase = [&]() {  // publish the wave's last values for the next phase of the wave above
+        if (W > 1) {
+            if (lane == 63) {
+                s_enew[wv] = lastnew;
+                s_eold[wv] = lastold;
+            }
+            __syncthreads();
+        }
     };
     const int nphase = nl - 1 + loops;
     if (nchunk == 1) {
         // one chunk per phase: a phase is short, so the noise is prefetched
         // four phases ahead through a four-slot register ring
         double r0[CH], r1[CH], r2[CH], r3[CH];
-        load_chunk(r0, 0 - lane, 0);
-        load_chunk(r1, 1 - lane, 0);
-        load_chunk(r2, 2 - lane, 0);
-        load_chunk(r3, 3 - lane, 0);
+        load_chunk(r0, 0 - g, 0);
+        load_chunk(r1, 1 - g, 0);
+        load_chunk(r2, 2 - g, 0);
+        load_chunk(r3, 3 - g, 0);
         auto phase = [&](int p, double (&slot)[CH]) {
             begin_phase();
-            run_chunk(p - lane, 0, slot);
-            load_chunk(slot, p + 4 - lane, 0);
+            run_chunk(p - g, 0, slot);
+            load_chunk(slot, p + 4 - g, 0);
+            end_phase();
         };
         for (int p = 0; p < nphase; p += 4) {
             phase(p, r0);
@@ -333,9 +360,9 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B,
     } else {
         // several chunks per phase: the next chunk is prefetched while this one computes
         double cur[CH], nxt[CH];
-        load_chunk(cur, -lane, 0);
+        load_chunk(cur, -g, 0);
         for (int p = 0; p < nphase; ++p) {
-            const int j = p - lane;
+            const int j = p - g;
             begin_phase();
             for (int c = 0; c < nchunk; ++c) {
                 if (c + 1 < nchunk) load_chunk(nxt, j, c + 1);
@@ -344,187 +371,12 @@ __global__ __launch_bounds__(64) void gs_sweep_kernel(const Qm1dGsArgs A, int B,
 #pragma unroll
                 for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
             }
+            end_phase();
         }
     }
 }
 
 // --------------------------------------------------------------- scan ----
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_min_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_max_i(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
-}
-__device__ __forceinline__ double wave_excl_max(double v, int lane) {  // max over lanes < lane
-    double incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double u = __shfl_up(incl, o, 64);
-        if (lane >= o) incl = fmax(incl, u);
-    }
-    const double ex = __shfl_up(incl, 1, 64);
-    return lane == 0 ? -__builtin_inf() : ex;
-}
-
-// LDS: f (previous step's field, the serial order's "old f"), n (this step),
-// d = |n - f - dw|, x, xx0 -- 5N doubles.
-__global__ __launch_bounds__(64) void gs_scan_kernel(const Qm1dGsArgs A) {
-    extern __shared__ double lds[];
-    const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
-    double *s_f = lds, *s_n = lds + N, *s_x = lds + 2 * N, *s_xx0 = lds + 3 * N, *s_d = lds + 4 * N;
-    const int lane = threadIdx.x;
-    const int B = (N + 63) / 64;
-    const int i0 = lane * B, i1 = min(N, i0 + B);
-    const double a = A.a, sig = A.sig;
-    const double NEG = -__builtin_inf();
-    for (int i = lane; i < N; i += 64) {
-        s_f[i] = A.f0[i];
-        s_x[i] = A.x0[i];
-        s_xx0[i] = A.xx00[i];
-    }
-    __syncthreads();
-    int E = A.st->lrgEl;
-    double V = A.st->lrgVl;
-    int brk_step = -1, brk_item = -1;
-    double w_next = A.om[0];
-    // B <= KP sites per lane: the next step's history row and noise are loaded
-    // into registers while this step is scanned (the loads' latency is then
-    // off the per-step critical path)
-    constexpr int KP = 16;
-    double pr[KP], px[KP];
-    auto prefetch = [&](int j) {
-        const double *row = A.hist + (size_t)j * N;
-        const double *xr = A.xi + (size_t)j * (N + 1);
-#pragma unroll
-        for (int b = 0; b < KP; ++b) {
-            const int i = i0 + b;
-            pr[b] = i < i1 ? row[i] : 0.;
-            px[b] = i < i1 ? xr[i] : 0.;
-        }
-    };
-    if (B <= KP) prefetch(0);
-    for (int j = 0; j < loops; ++j) {
-        const double w = w_next;
-        if (j + 1 < loops) w_next = A.om[j + 1];  // in flight during this step
-        const double *row = A.hist + (size_t)j * N;
-        const double *xr = A.xi + (size_t)j * (N + 1);
-        // nf[E] as the serial order sees it before item E runs this step:
-        // the previous step's value (the persistent newf buffer at j = 0)
-        const double nfE = j == 0 ? A.nfp[E] : s_f[E];
-        const double T0 = nfE + xcl((double)E * a, w, pot);
-        // this step's global inputs, staged once
-        if (B <= KP) {
-#pragma unroll
-            for (int b = 0; b < KP; ++b) {
-                const int i = i0 + b;
-                if (i < i1) {
-                    s_n[i] = pr[b];
-                    s_d[i] = absol(pr[b] - s_f[i] - sig * px[b]);  // :139, |nf - f - dw|
-                }
-            }
-            if (j + 1 < loops) prefetch(j + 1);
-        } else {
-#pragma unroll 4
-            for (int i = i0; i < i1; ++i) {
-                const double v = row[i];
-                s_n[i] = v;
-                s_d[i] = absol(v - s_f[i] - sig * xr[i]);  // :139, |nf - f - dw|
-            }
-        }
-        double m1 = NEG;
-        for (int i = i0; i < min(i1, E); ++i) m1 = fmax(m1, s_n[i] + xcl((double)i * a, w, pot));
-        __syncthreads();
-        const bool caseB = wave_max(m1) > T0;  // a leader before E: no reset at item E
-        // lane totals of Y (X, masked below E in case A) and |X|
-        double ty = NEG, ta = NEG;
-        for (int i = i0; i < i1; ++i) {
-            const double X = s_n[i] + xcl((double)i * a, w, pot);
-            if (caseB || i >= E) ty = fmax(ty, X);
-            ta = fmax(ta, absol(X));
-        }
-        double py = wave_excl_max(ty, lane), pa = wave_excl_max(ta, lane);
-        const double base = caseB ? T0 : NEG;
-        int first_bad = 0x7fffffff, last_lead = -1;
-        double Vbad = 0.;
-        for (int i = i0; i < i1; ++i) {
-            const double X = s_n[i] + xcl((double)i * a, w, pot);
-            const double th = fmax(base, py);
-            const bool lead = (caseB || i > E) && X > th;
-            const double Vi = fmax(V, pa);  // V seen by item i (max over k < i)
-            if (lead) {
-                last_lead = i;
-                if (s_d[i] > Vi && i < first_bad) {
-                    first_bad = i;
-                    Vbad = fmax(Vi, absol(X));
-                }
-            }
-            if (caseB || i >= E) py = fmax(py, X);
-            pa = fmax(pa, absol(X));
-        }
-        const int kb = wave_min_i(first_bad);
-        if (kb != 0x7fffffff && j > 0) {  // items after kb see stable != 1 and never run this round
-            E = kb;
-            V = __shfl(Vbad, kb / B, 64);
-            brk_step = j;
-            brk_item = kb;
-            break;
-        }
-        const int ll = wave_max_i(last_lead);
-        if (ll >= 0) E = ll;
-        V = fmax(V, wave_max(ta));
-        if (kb != 0x7fffffff) {  // round 0: the stable test only starts at round 1 (:168-171), all items ran
-            brk_step = 0;
-            brk_item = N;
-            break;
-        }
-        // running means, :144-145 (f[i] old; f[mid] already updated for i > mid
-        // except in the last step, which commits nothing)
-        const double den = (double)(A.runs + j + 1);
-        const double xm = xcl((double)mid * a, w, pot);
-        const double fm_old = s_f[mid], fm_new = s_n[mid];
-        for (int i = i0; i < i1; ++i) {
-            const double g = s_f[i] + xcl((double)i * a, w, pot);
-            const double fm = (i > mid && j < loops - 1) ? fm_new : fm_old;
-            s_xx0[i] = s_xx0[i] + (g * (fm + xm) - s_xx0[i]) / den;
-            s_x[i] = s_x[i] + (g - s_x[i]) / den;
-        }
-        __syncthreads();
-        for (int i = i0; i < i1; ++i) s_f[i] = s_n[i];
-        __syncthreads();
-    }
-    // persistent newf (never rolled back by the host): the last value each item wrote
-    if (brk_step < 0) {
-        for (int i = i0; i < i1; ++i) {
-            A.nf[i] = s_f[i];
-            A.nfp[i] = s_f[i];
-            A.nx[i] = s_x[i];
-            A.nxx0[i] = s_xx0[i];
-        }
-    } else {
-        for (int i = i0; i < i1; ++i)
-            if (i <= brk_item) A.nfp[i] = s_n[i];
-            else if (brk_step > 0) A.nfp[i] = s_f[i];  // still the previous round's value
-    }
-    if (lane == 0) {
-        A.st->lrgEl = E;
-        A.st->lrgVl = V;
-        A.st->stable = brk_step < 0 ? 1 : 0;
-        A.st->steps_done = brk_step < 0 ? loops : brk_step + 1;
-        A.st->omega_out = A.om[loops];
-        A.st->consumed = brk_step < 0 ? (long long)loops * (N + 1)
-                                      : (long long)brk_step * (N + 1) + brk_item + 1;
-    }
-}
-
 // ------------------------------------------------- scan, register path ----
 // Wave-wide max-scans by DPP (row_shr 1/2/4/8, row_bcast 15/31: the gfx9
 // inclusive-scan sequence), no LDS round trips; 64-bit values move as two
@@ -572,7 +424,7 @@ __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v);
 // N <= 64 KB: the lane's KB sites stay in registers (field, running means,
 // this step's X, |X|, drift check), the next step's inputs are prefetched, and
 // only f / nf go through LDS for the cross-lane reads of nf[E] and f[mid].
-// Same semantics and expression order as gs_scan_kernel.
+// The stability scan of one step as prefix maxima.
 template <int KB>
 __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
     extern __shared__ double lds[];
@@ -729,13 +581,204 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
     }
 }
 
+// --------------------------------------------- scan, several waves ----
+// N > 128: W waves (<= 16), KB sites per thread in registers; the wave-level
+// DPP scans are joined across waves through LDS (four barriers per step).
+// Same semantics and expression order as gs_scan_reg_kernel.
+template <int KB>
+__global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
+    extern __shared__ double lds[];
+    __shared__ double s_m1[16], s_ta[16], s_ty[16], s_vbad;
+    __shared__ int s_fb[16], s_ll[16];
+    const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
+    double *s_f = lds, *s_n = lds + N;
+    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
+    const int B = (N + blockDim.x - 1) / blockDim.x;
+    const int i0 = g * B, i1 = min(N, i0 + B);
+    const double a = A.a, sig = A.sig;
+    const double NEG = -__builtin_inf();
+    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB];
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+        const int i = i0 + b;
+        const bool in = b < B && i < i1;
+        f_[b] = in ? A.f0[i] : 0.;
+        x_[b] = in ? A.x0[i] : 0.;
+        xx_[b] = in ? A.xx00[i] : 0.;
+        if (in) s_f[i] = f_[b];
+    }
+    auto prefetch = [&](int j) {
+        const double *row = A.hist + (size_t)j * N;
+        const double *xr = A.xi + (size_t)j * (N + 1);
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            const bool in = b < B && i < i1;
+            pr[b] = in ? row[i] : 0.;
+            px[b] = in ? xr[i] : 0.;
+        }
+    };
+    prefetch(0);
+    __syncthreads();
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int brk_step = -1, brk_item = -1;
+    double w_next = A.om[0];
+    double n[KB];
+    for (int j = 0; j < loops; ++j) {
+        const double w = w_next;
+        if (j + 1 < loops) w_next = A.om[j + 1];
+        double X[KB], D[KB], xc[KB];
+        double m1 = NEG, ta = NEG;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            n[b] = pr[b];
+            xc[b] = xcl((double)i * a, w, pot);
+            X[b] = n[b] + xc[b];
+            D[b] = absol(n[b] - f_[b] - sig * px[b]);  // :139, |nf - f - dw|
+            if (b < B && i < i1) {
+                s_n[i] = n[b];
+                if (i < E) m1 = fmax(m1, X[b]);
+                ta = fmax(ta, absol(X[b]));
+            }
+        }
+        if (j + 1 < loops) prefetch(j + 1);
+        const double ta_wex = dpp_excl_max(ta);
+        {
+            const double m1w = dpp_all_max(m1), taw = dpp_all_max(ta);
+            if (lane == 0) {
+                s_m1[wv] = m1w;
+                s_ta[wv] = taw;
+            }
+        }
+        __syncthreads();  // #1: s_n, wave maxima of X below E and of |X|
+        const double nfE = j == 0 ? A.nfp[E] : s_f[E];
+        const double T0 = nfE + xcl((double)E * a, w, pot);
+        double M1 = NEG, ta_pre = NEG, ta_all = NEG;
+        for (int k = 0; k < W; ++k) {
+            M1 = fmax(M1, s_m1[k]);
+            ta_all = fmax(ta_all, s_ta[k]);
+            if (k < wv) ta_pre = fmax(ta_pre, s_ta[k]);
+        }
+        const bool caseB = M1 > T0;  // a leader before E: no reset at item E
+        double ty = NEG;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            if (b < B && i < i1 && (caseB || i >= E)) ty = fmax(ty, X[b]);
+        }
+        const double ty_wex = dpp_excl_max(ty);
+        {
+            const double tyw = dpp_all_max(ty);
+            if (lane == 0) s_ty[wv] = tyw;
+        }
+        __syncthreads();  // #2: wave maxima of Y
+        double ty_pre = NEG;
+        for (int k = 0; k < wv; ++k) ty_pre = fmax(ty_pre, s_ty[k]);
+        double py = fmax(ty_pre, ty_wex), pa = fmax(ta_pre, ta_wex);
+        const double base = caseB ? T0 : NEG;
+        int first_bad = 0x7fffffff, last_lead = -1;
+        double Vbad = 0.;
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            if (b < B && i < i1) {
+                const double th = fmax(base, py);
+                const bool lead = (caseB || i > E) && X[b] > th;
+                const double Vi = fmax(V, pa);  // V seen by item i (max over k < i)
+                if (lead) {
+                    last_lead = i;
+                    if (D[b] > Vi && i < first_bad) {
+                        first_bad = i;
+                        Vbad = fmax(Vi, absol(X[b]));
+                    }
+                }
+                if (caseB || i >= E) py = fmax(py, X[b]);
+                pa = fmax(pa, absol(X[b]));
+            }
+        }
+        {
+            const int fbw = dpp_all_min_i(first_bad), llw = dpp_all_max_i(last_lead);
+            if (lane == 0) {
+                s_fb[wv] = fbw;
+                s_ll[wv] = llw;
+            }
+        }
+        __syncthreads();  // #3: wave first-unstable / last-leader items
+        int kb = 0x7fffffff, ll = -1;
+        for (int k = 0; k < W; ++k) {
+            kb = min(kb, s_fb[k]);
+            ll = max(ll, s_ll[k]);
+        }
+        if (kb != 0x7fffffff && j > 0) {  // items after kb see stable != 1 and never run this round
+            if (first_bad == kb) s_vbad = Vbad;
+            __syncthreads();
+            E = kb;
+            V = s_vbad;
+            brk_step = j;
+            brk_item = kb;
+            break;
+        }
+        if (ll >= 0) E = ll;
+        V = fmax(V, ta_all);
+        if (kb != 0x7fffffff) {  // round 0: the stable test only starts at round 1 (:168-171)
+            brk_step = 0;
+            brk_item = N;
+            break;
+        }
+        const double den = (double)(A.runs + j + 1);
+        const double xm = xcl((double)mid * a, w, pot);
+        const double fm_old = s_f[mid], fm_new = s_n[mid];
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            const double gg = f_[b] + xc[b];
+            const double fm = (i > mid && j < loops - 1) ? fm_new : fm_old;
+            xx_[b] = xx_[b] + (gg * (fm + xm) - xx_[b]) / den;
+            x_[b] = x_[b] + (gg - x_[b]) / den;
+        }
+        __syncthreads();  // #4: every read of s_f (E, mid) done before it is overwritten
+#pragma unroll
+        for (int b = 0; b < KB; ++b) {
+            const int i = i0 + b;
+            f_[b] = n[b];
+            if (b < B && i < i1) s_f[i] = n[b];
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+        const int i = i0 + b;
+        if (!(b < B && i < i1)) continue;
+        if (brk_step < 0) {
+            A.nf[i] = f_[b];
+            A.nfp[i] = f_[b];
+            A.nx[i] = x_[b];
+            A.nxx0[i] = xx_[b];
+        } else if (i <= brk_item) {
+            A.nfp[i] = n[b];
+        } else if (brk_step > 0) {
+            A.nfp[i] = f_[b];  // still the previous round's value
+        }
+    }
+    if (g == 0) {
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = brk_step < 0 ? 1 : 0;
+        A.st->steps_done = brk_step < 0 ? loops : brk_step + 1;
+        A.st->omega_out = A.om[loops];
+        A.st->consumed = brk_step < 0 ? (long long)loops * (N + 1)
+                                      : (long long)brk_step * (N + 1) + brk_item + 1;
+    }
+}
+
 }  // namespace
 
 constexpr int kSweepLdsMax = 96 * 1024;
 
-int qm1d_gs_block(int N) {
+int qm1d_gs_block(int N) {  // sites per pipeline lane: 2 while <= 1024 lanes (16 waves) suffice
     if (N < 2 || N > kQm1dGsMaxN) return 0;
-    return N <= 128 ? 2 : (N + 63) / 64;
+    return std::max(2, (N + 1023) / 1024);
 }
 
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
@@ -749,7 +792,7 @@ hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, 
 hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const int B = qm1d_gs_block(a.N);
     if (B == 0) return hipErrorInvalidValue;
-    const size_t lds1 = sizeof(double) * (size_t)a.N, lds5 = 5 * lds1;
+    const size_t lds1 = sizeof(double) * (size_t)a.N;
     // the dynamic-LDS limit is a per-device function attribute: set it once per device
     static bool attr_set[64] = {};
     int dev = 0;
@@ -757,8 +800,8 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     bool &attr = attr_set[dev];
     if (!attr) {
         hipError_t e;
-        if ((e = hipFuncSetAttribute((const void *)gs_scan_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)(5 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+        if ((e = hipFuncSetAttribute((const void *)gs_scan_mw_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)(2 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
             return e;
         for (const void *k : {(const void *)gs_sweep_kernel<2>, (const void *)gs_sweep_kernel<8>})
             if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kSweepLdsMax)) != hipSuccess)
@@ -770,15 +813,19 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const size_t lds_om = sizeof(double) * ((size_t)a.N + a.loops + 1);
     const int om_lds = lds_om <= (size_t)kSweepLdsMax ? 1 : 0;
     const size_t lds_sw = om_lds ? lds_om : lds1;
-    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(64), lds_sw, s, a, B, om_lds);
-    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(64), lds_sw, s, a, B, om_lds);
-    const int B3 = (a.N + 63) / 64;
+    const int nl = (a.N + B - 1) / B;
+    const int threads = 64 * ((nl + 63) / 64);  // one pipeline lane per thread, <= 1024
+    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(threads), lds_sw, s, a, B, om_lds);
+    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(threads), lds_sw, s, a, B, om_lds);
     const size_t lds2 = 2 * lds1;
-    if (B3 <= 2) hipLaunchKernelGGL(gs_scan_reg_kernel<2>, dim3(1), dim3(64), lds2, s, a);
-    else if (B3 <= 4) hipLaunchKernelGGL(gs_scan_reg_kernel<4>, dim3(1), dim3(64), lds2, s, a);
-    else if (B3 <= 8) hipLaunchKernelGGL(gs_scan_reg_kernel<8>, dim3(1), dim3(64), lds2, s, a);
-    else if (B3 <= 16) hipLaunchKernelGGL(gs_scan_reg_kernel<16>, dim3(1), dim3(64), lds2, s, a);
-    else hipLaunchKernelGGL(gs_scan_kernel, dim3(1), dim3(64), lds5, s, a);
+    if (a.N <= 128) {
+        hipLaunchKernelGGL(gs_scan_reg_kernel<2>, dim3(1), dim3(64), lds2, s, a);
+    } else if (a.N <= 256) {  // one wave without barriers still beats two waves here (measured)
+        hipLaunchKernelGGL(gs_scan_reg_kernel<4>, dim3(1), dim3(64), lds2, s, a);
+    } else {  // 2 sites per thread up to 2048 sites (16 waves), up to 4 beyond
+        const int waves = std::min(16, (a.N + 127) / 128);
+        hipLaunchKernelGGL(gs_scan_mw_kernel<4>, dim3(1), dim3(64 * waves), lds2, s, a);
+    }
     return hipGetLastError();
 }
 

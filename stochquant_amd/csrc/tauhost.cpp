@@ -18,7 +18,7 @@
 // same arguments (run_phi4 below).
 // SQ_ORDER=serial selects the reference's own serial order instead
 // (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
-// SQ_ORDER_SERIAL in stochquant.h), N <= 3072.
+// SQ_ORDER_SERIAL in stochquant.h), N <= 4096.
 #include <chrono>
 #include <cmath>
 #include <cstdio>

@@ -82,7 +82,7 @@ def _exact(res):
 @pytest.mark.parametrize("N,loops,dtau", [(2, 3, 0.01), (3, 1, 0.01), (4, 2, 0.01), (5, 7, 0.02),
                                           (63, 20, 0.01), (64, 20, 0.01), (65, 9, 0.01), (100, 50, 0.002),
                                           (129, 13, 0.01), (200, 40, 0.004), (1000, 8, 0.001),
-                                          (3072, 3, 0.001)])
+                                          (3072, 3, 0.001), (4096, 2, 0.001)])
 def test_injected_noise_frames_bitwise_pot0(gpu, oracle_mod, N, loops, dtau):
     rng = np.random.default_rng(N)
     f0 = 0.3 * rng.standard_normal(N)
@@ -137,7 +137,7 @@ def test_double_well_within_tanh_tolerance(gpu, oracle_mod):
 
 def test_serial_order_rejects_large_n(gpu):
     from stochquant_amd import Qm1dChain, StochQuantError
-    with Qm1dChain(3073, 0.1, 0.001, pot=0, loops=2) as g:
+    with Qm1dChain(4097, 0.1, 0.001, pot=0, loops=2) as g:
         with pytest.raises(StochQuantError):
             g.set_ordering("serial")
 
