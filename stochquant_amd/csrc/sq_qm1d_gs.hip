@@ -655,12 +655,10 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
         __syncthreads();  // #1: s_n, wave maxima of X below E and of |X|
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
         const double T0 = nfE + xcl((double)E * a, w, pot);
-        double M1 = NEG, ta_pre = NEG, ta_all = NEG;
-        for (int k = 0; k < W; ++k) {
-            M1 = fmax(M1, s_m1[k]);
-            ta_all = fmax(ta_all, s_ta[k]);
-            if (k < wv) ta_pre = fmax(ta_pre, s_ta[k]);
-        }
+        // lane k reads wave k's partial: one LDS load and a DPP reduction per quantity
+        const double M1 = dpp_all_max(lane < W ? s_m1[lane] : NEG);
+        const double ta_all = dpp_all_max(lane < W ? s_ta[lane] : NEG);
+        const double ta_pre = dpp_all_max(lane < wv ? s_ta[lane] : NEG);
         const bool caseB = M1 > T0;  // a leader before E: no reset at item E
         double ty = NEG;
 #pragma unroll
@@ -674,8 +672,7 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
             if (lane == 0) s_ty[wv] = tyw;
         }
         __syncthreads();  // #2: wave maxima of Y
-        double ty_pre = NEG;
-        for (int k = 0; k < wv; ++k) ty_pre = fmax(ty_pre, s_ty[k]);
+        const double ty_pre = dpp_all_max(lane < wv ? s_ty[lane] : NEG);
         double py = fmax(ty_pre, ty_wex), pa = fmax(ta_pre, ta_wex);
         const double base = caseB ? T0 : NEG;
         int first_bad = 0x7fffffff, last_lead = -1;
@@ -706,11 +703,8 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
             }
         }
         __syncthreads();  // #3: wave first-unstable / last-leader items
-        int kb = 0x7fffffff, ll = -1;
-        for (int k = 0; k < W; ++k) {
-            kb = min(kb, s_fb[k]);
-            ll = max(ll, s_ll[k]);
-        }
+        const int kb = dpp_all_min_i(lane < W ? s_fb[lane] : 0x7fffffff);
+        const int ll = dpp_all_max_i(lane < W ? s_ll[lane] : -1);
         if (kb != 0x7fffffff && j > 0) {  // items after kb see stable != 1 and never run this round
             if (first_bad == kb) s_vbad = Vbad;
             __syncthreads();
