@@ -193,9 +193,11 @@ int sq_selftest_dpp(int device, float *out64x2);
 int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
 int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps);
 /* The serial order's draws of one full launch from `seed` on the device:
- * words t1>>16, t2>>16, the seed after each call, xi ((N+1)*loops each). */
+ * words t1>>16, t2>>16, the seed after each call, xi ((N+1)*loops each).
+ * generator 1 = the grid-wide generator the frames use, 0 = the one-block
+ * generator it falls back to from the first exceptional call. */
 int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
-                    unsigned int *w2, unsigned long long *seeds, double *xi);
+                    unsigned int *w2, unsigned long long *seeds, double *xi, int generator);
 
 #ifdef __cplusplus
 }

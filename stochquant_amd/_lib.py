@@ -104,7 +104,8 @@ SIGNATURES = {
     "sq_qm1d_noise_consumed": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
     "sq_selftest_lcg": (ctypes.c_int, [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
-                                       ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_double)]),
+                                       ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.c_int]),
     "sq_set_dtau": (ctypes.c_int, [_P, ctypes.c_double]),
     "sq_get_dtau": (ctypes.c_int, [_P, _D]),
     "sq_get_step": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),

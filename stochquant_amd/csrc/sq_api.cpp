@@ -110,6 +110,7 @@ struct sq_ctx {
     double *g_xi = nullptr, *g_om = nullptr, *g_hist_buf = nullptr, *g_nfp = nullptr;
     uint32_t *g_w1 = nullptr, *g_w2 = nullptr;
     unsigned long long *g_seeds = nullptr;
+    unsigned long long *g_lcg_scr = nullptr;  // grid-wide LCG generator scratch (sq::kLcgScratch words)
     sq::Qm1dGsState *g_st = nullptr;
     // PHI4
     int Lx = 0, Ly = 0;
@@ -622,6 +623,7 @@ int gs_reserve(sq_ctx *c) {
         SQ_HIP(hipMalloc(&c->g_seeds, sizeof(unsigned long long) * calls));
         c->g_calls = calls;
     }
+    if (c->g_lcg_scr == nullptr) SQ_HIP(hipMalloc(&c->g_lcg_scr, sizeof(unsigned long long) * sq::kLcgScratch));
     if (hist > c->g_hist) {
         (void)hipFree(c->g_hist_buf);
         (void)hipFree(c->g_om);
@@ -650,7 +652,7 @@ int qm1d_gs_frame(sq_ctx *c, int *stable) {
     if (rc) return rc;
     if (!injected)
         SQ_HIP(sq::qm1d_gs_lcg_launch(c->lcg_seed, c->N, calls, c->g_w1, c->g_w2, c->g_seeds, c->g_xi,
-                                      c->qstream));
+                                      c->g_lcg_scr, c->qstream));
     sq::Qm1dGsArgs a{};
     const int k = c->qcur;
     a.f0 = c->qf[k];
@@ -900,6 +902,7 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->g_w1);
     (void)hipFree(c->g_w2);
     (void)hipFree(c->g_seeds);
+    (void)hipFree(c->g_lcg_scr);
     (void)hipFree(c->g_st);
     (void)hipFree(c->flag);
     (void)hipFree(c->dacc);
@@ -1331,18 +1334,19 @@ int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int
 }
 
 int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
-                    unsigned int *w2, unsigned long long *seeds, double *xi) {
+                    unsigned int *w2, unsigned long long *seeds, double *xi, int generator) {
     if (!w1 || !w2 || !seeds || !xi || N < 1 || loops < 1) return fail(SQ_E_ARG, "bad argument");
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
     DeviceGuard g(device);
     const long long n = (long long)(N + 1) * loops;
     char *d = nullptr;
-    SQ_HIP(hipMalloc(&d, (size_t)n * 24));
+    SQ_HIP(hipMalloc(&d, (size_t)n * 24 + 8 * sq::kLcgScratch));
     uint32_t *dw1 = (uint32_t *)d, *dw2 = dw1 + n;
     unsigned long long *ds = (unsigned long long *)(dw2 + n);
     double *dx = (double *)(ds + n);
-    hipError_t e = sq::qm1d_gs_lcg_launch(seed, N, n, dw1, dw2, ds, dx, nullptr);
+    unsigned long long *scr = generator == 1 ? (unsigned long long *)(dx + n) : nullptr;
+    hipError_t e = sq::qm1d_gs_lcg_launch(seed, N, n, dw1, dw2, ds, dx, scr, nullptr);
     if (e == hipSuccess) e = hipMemcpy(w1, dw1, n * 4, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(w2, dw2, n * 4, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(seeds, ds, n * 8, hipMemcpyDeviceToHost);

@@ -107,8 +107,14 @@ struct Qm1dGsArgs {
 
 constexpr int kQm1dGsMaxN = 4096;  // <= 4 sites per thread of a 1024-thread block; 2N doubles of LDS
 int qm1d_gs_block(int N);  // sites per lane of the sweep pipeline, 0 if N unsupported
+// The LCG stream of a launch: w1/w2/seeds/xi per call.  scr (kLcgScratch
+// words, or null for the one-block generator) holds the grid-wide
+// generator's chunk maps and start seeds.
+constexpr int kLcgChunks = 16384;
+constexpr size_t kLcgScratch = 3 * (size_t)kLcgChunks + 1;
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
-                              uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s);
+                              uint32_t *w2, unsigned long long *seeds, double *xi,
+                              unsigned long long *scr, hipStream_t s);
 hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s);
 
 // -------------------------------------------------------------- selftest --

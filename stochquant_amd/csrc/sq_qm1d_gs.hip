@@ -113,15 +113,106 @@ __device__ __forceinline__ LcgCall lcg_exact(uint64_t s, uint64_t g) {  // the r
 
 constexpr int kLcgThreads = 1024;
 
+// The common path is three grid-wide kernels over kLcgChunks contiguous
+// chunks of calls: compose each chunk's case-Q map, scan the maps (one
+// block), replay each chunk from its start seed (recording the first
+// exceptional call).  gs_lcg_kernel (one block) then resumes exactly from
+// that call -- it returns at once when there was none.
+// scr: maps a[T], b[T], chunk start seeds[T], first exceptional call.
+
+__device__ __forceinline__ void lcg_chunk(long long ncalls, int t, long long &kb, long long &ke) {
+    const long long C = (ncalls + kLcgChunks - 1) / kLcgChunks;
+    kb = min(ncalls, (long long)t * C);
+    ke = min(ncalls, kb + C);
+}
+
+__global__ __launch_bounds__(256) void gs_lcg_compose_kernel(int N, long long ncalls, unsigned long long *scr) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t == 0) scr[3 * kLcgChunks] = (unsigned long long)ncalls;
+    long long kb, ke;
+    lcg_chunk(ncalls, t, kb, ke);
+    const uint64_t np1 = (uint64_t)N + 1;
+    uint64_t a = 1, b = 0, g = (uint64_t)kb % np1;
+    for (long long k = kb; k < ke; ++k) {
+        a = (kAlpha * a) & kM48;
+        b = (kAlpha * b + lcg_beta(g)) & kM48;
+        g = g + 1 == np1 ? 0 : g + 1;
+    }
+    scr[t] = a;
+    scr[kLcgChunks + t] = b;
+}
+
+__global__ __launch_bounds__(1024) void gs_lcg_scan_kernel(unsigned long long seed, unsigned long long *scr) {
+    constexpr int PER = kLcgChunks / 1024;
+    __shared__ uint64_t sa[1024], sb[1024];
+    const int t = threadIdx.x;
+    uint64_t a = 1, b = 0;
+    for (int i = 0; i < PER; ++i) {  // my PER consecutive maps, composed in call order
+        const uint64_t am = scr[t * PER + i], bm = scr[kLcgChunks + t * PER + i];
+        b = (am * b + bm) & kM48;
+        a = (am * a) & kM48;
+    }
+    sa[t] = a;
+    sb[t] = b;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        uint64_t pa = 1, pb = 0;
+        if (t >= o) {
+            pa = sa[t - o];
+            pb = sb[t - o];
+        }
+        __syncthreads();
+        if (t >= o) {
+            const uint64_t na = (sa[t] * pa) & kM48, nb = (sa[t] * pb + sb[t]) & kM48;
+            sa[t] = na;
+            sb[t] = nb;
+        }
+        __syncthreads();
+    }
+    // chunk 0 starts from the exact u64 seed; later chunks from its residue image
+    uint64_t s = t == 0 ? seed : ((sa[t - 1] * (seed & kM48) + sb[t - 1]) & kM48);
+    for (int i = 0; i < PER; ++i) {
+        const int m = t * PER + i;
+        scr[2 * kLcgChunks + m] = s;
+        s = (scr[m] * (s & kM48) + scr[kLcgChunks + m]) & kM48;
+    }
+}
+
+__global__ __launch_bounds__(256) void gs_lcg_replay_kernel(int N, long long ncalls, uint32_t *w1, uint32_t *w2,
+                                                            unsigned long long *seeds,
+                                                            unsigned long long *scr) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    long long kb, ke;
+    lcg_chunk(ncalls, t, kb, ke);
+    const uint64_t np1 = (uint64_t)N + 1;
+    uint64_t s = scr[2 * kLcgChunks + t], g = (uint64_t)kb % np1;
+    for (long long k = kb; k < ke; ++k) {
+        const LcgCall c = lcg_case_q(s, g);
+        g = g + 1 == np1 ? 0 : g + 1;
+        if (c.exc) {
+            atomicMin(&scr[3 * kLcgChunks], (unsigned long long)k);
+            break;
+        }
+        w1[k] = (uint32_t)(c.t1 >> 16);
+        w2[k] = (uint32_t)(c.t2 >> 16);
+        seeds[k] = c.s;
+        s = c.s;
+    }
+}
+
+// One block from call *kstart on (all calls when kstart is null): the same
+// compose / scan / replay in a loop, with the exceptional call done exactly.
 __global__ __launch_bounds__(kLcgThreads) void gs_lcg_kernel(unsigned long long seed, int N, long long ncalls,
                                                               uint32_t *w1, uint32_t *w2,
-                                                              unsigned long long *seeds) {
+                                                              unsigned long long *seeds,
+                                                              const unsigned long long *kstart) {
     __shared__ uint64_t sa[kLcgThreads], sb[kLcgThreads];
     __shared__ long long s_exc;
     const int t = threadIdx.x;
     const uint64_t np1 = (uint64_t)N + 1;
-    long long k0 = 0;
-    uint64_t s_in = seed;  // exact seed before call k0
+    long long k0 = kstart ? (long long)*kstart : 0;
+    if (k0 >= ncalls) return;
+    uint64_t s_in = k0 == 0 ? seed : seeds[k0 - 1];  // exact seed before call k0
     while (k0 < ncalls) {
         const long long n = ncalls - k0;
         const long long C = (n + kLcgThreads - 1) / kLcgThreads;
@@ -776,8 +867,19 @@ int qm1d_gs_block(int N) {  // sites per pipeline lane: 2 while <= 1024 lanes (1
 }
 
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
-                              uint32_t *w2, unsigned long long *seeds, double *xi, hipStream_t s) {
-    hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(kLcgThreads), 0, s, seed, N, ncalls, w1, w2, seeds);
+                              uint32_t *w2, unsigned long long *seeds, double *xi,
+                              unsigned long long *scr, hipStream_t s) {
+    if (scr == nullptr) {  // one block, all calls
+        hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(kLcgThreads), 0, s, seed, N, ncalls, w1, w2, seeds,
+                           (const unsigned long long *)nullptr);
+    } else {
+        constexpr int blocks = kLcgChunks / 256;
+        hipLaunchKernelGGL(gs_lcg_compose_kernel, dim3(blocks), dim3(256), 0, s, N, ncalls, scr);
+        hipLaunchKernelGGL(gs_lcg_scan_kernel, dim3(1), dim3(1024), 0, s, seed, scr);
+        hipLaunchKernelGGL(gs_lcg_replay_kernel, dim3(blocks), dim3(256), 0, s, N, ncalls, w1, w2, seeds, scr);
+        hipLaunchKernelGGL(gs_lcg_kernel, dim3(1), dim3(kLcgThreads), 0, s, seed, N, ncalls, w1, w2, seeds,
+                           (const unsigned long long *)(scr + 3 * kLcgChunks));
+    }
     const int blocks = (int)std::min<long long>(2048, (ncalls + 255) / 256);
     hipLaunchKernelGGL(gs_xi_kernel, dim3(blocks), dim3(256), 0, s, w1, w2, xi, ncalls);
     return hipGetLastError();

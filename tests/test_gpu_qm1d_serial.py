@@ -18,7 +18,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_lcg(sqlib, seed, N, loops):
+def _gpu_lcg(sqlib, seed, N, loops, generator=1):
     import ctypes
     n = (N + 1) * loops
     w1 = np.empty(n, dtype=np.uint32)
@@ -27,15 +27,16 @@ def _gpu_lcg(sqlib, seed, N, loops):
     xi = np.empty(n)
     P = lambda a, t: a.ctypes.data_as(ctypes.POINTER(t))
     rc = sqlib.sq_selftest_lcg(0, seed, N, loops, P(w1, ctypes.c_uint), P(w2, ctypes.c_uint),
-                               P(seeds, ctypes.c_ulonglong), P(xi, ctypes.c_double))
+                               P(seeds, ctypes.c_ulonglong), P(xi, ctypes.c_double), generator)
     assert rc == 0
     return xi, w1, w2, seeds
 
 
+@pytest.mark.parametrize("generator", [0, 1])
 @pytest.mark.parametrize("seed,N,loops", [(12345, 4, 2), (1804289383, 100, 30), (7, 3, 500),
                                           (2 ** 31 - 3, 1000, 4), (1804289383, 999, 1000)])
-def test_lcg_stream_matches_reference(gpu, sqlib, oracle_mod, seed, N, loops):
-    xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, N, loops)
+def test_lcg_stream_matches_reference(gpu, sqlib, oracle_mod, seed, N, loops, generator):
+    xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, N, loops, generator)
     rxi, rw1, rw2, rseeds = oracle_mod.ref_noise_stream(seed, N, loops)
     assert np.array_equal(w1, rw1) and np.array_equal(w2, rw2) and np.array_equal(seeds, rseeds)
     assert np.all(np.abs(xi - rxi) <= 2.5e-7 * np.abs(rxi) + 1e-7)
@@ -142,7 +143,8 @@ def test_serial_order_rejects_large_n(gpu):
             g.set_ordering("serial")
 
 
-def test_lcg_exceptional_calls(gpu, sqlib, oracle_mod):
+@pytest.mark.parametrize("generator", [0, 1])
+def test_lcg_exceptional_calls(gpu, sqlib, oracle_mod, generator):
     """Seeds that drive the rare branches of random(): case P (s < 2^31 and
     t2 < 2^31 -> s + t2) and the u64 wrap of t2 - 2^31.  The parallel-prefix
     generator's exact fix-up must reproduce the serial chain bit for bit."""
@@ -159,6 +161,46 @@ def test_lcg_exceptional_calls(gpu, sqlib, oracle_mod):
                 break
     assert found
     for seed in found:
-        xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, 7, 300)
+        xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, 7, 300, generator)
         rxi, rw1, rw2, rseeds = oracle_mod.ref_noise_stream(seed, 7, 300)
+        assert np.array_equal(w1, rw1) and np.array_equal(w2, rw2) and np.array_equal(seeds, rseeds)
+
+
+_M48 = (1 << 48) - 1
+_A, _B = 0x5DEECE66D, 0xB
+
+
+def _seed_reaching(s_k, k, N):
+    """The seed whose case-Q chain (s' = A^2 s + beta(g), the common branch of
+    tau_kernel.cl:269-284) is s_k before call k: the chain run backwards."""
+    alpha = _A * _A & _M48
+    ainv = pow(alpha, -1, 1 << 48)
+    s = s_k
+    for j in range(k - 1, -1, -1):
+        g = j % (N + 1)
+        beta = (_A * _A * g + _A * _B + _A * g + _B - 2 ** 31) & _M48
+        s = ainv * (s - beta) & _M48
+    return s
+
+
+@pytest.mark.parametrize("kind,k", [("retry", 500_123), ("retry", 16_000), ("retry", 999_999),
+                                    ("case_p", 333_333), ("case_p", 61)])
+def test_lcg_exception_mid_stream(gpu, sqlib, oracle_mod, kind, k):
+    """An exceptional call deep inside a 10^6-call launch (constructed by
+    running the chain backwards from a state that takes it): the isinf retry
+    (t1 >> 16 == 0) or case P (s < 2^31 and t2 < 2^31).  The grid-wide
+    generator's chunks after it are invalid; the one-block resume from the
+    first exceptional call must give the serial chain bit for bit."""
+    N, loops = 999, 1000
+    g = k % (N + 1)
+    if kind == "retry":
+        s_k = ((12345 - _B) * pow(_A, -1, 1 << 48) - g) & _M48  # t1 = 12345 -> t1 >> 16 == 0
+    else:
+        s_k = next(s for s in range(1, 1 << 31)
+                   if ((((s + g) * _A + _B) & _M48) + g) * _A + _B & _M48 < 2 ** 31)
+    seed = _seed_reaching(s_k, k, N)
+    rxi, rw1, rw2, rseeds = oracle_mod.ref_noise_stream(seed, N, loops)
+    assert int(rseeds[k - 1]) & _M48 == s_k  # the construction reached the state
+    for generator in (1, 0):
+        xi, w1, w2, seeds = _gpu_lcg(sqlib, seed, N, loops, generator)
         assert np.array_equal(w1, rw1) and np.array_equal(w2, rw2) and np.array_equal(seeds, rseeds)
