@@ -106,7 +106,8 @@ struct sq_ctx {
     unsigned long long lcg_seed = 0;  // rand1 (tauhost.c:185), advanced by the calls each frame makes
     bool inject_pending = false;       // g_xi holds a caller-supplied stream for the next frame
     unsigned long long consumed = 0;   // random() calls of the last serial frame
-    long long g_calls = 0, g_hist = 0; // capacities
+    long long g_calls = 0, g_hist = 0, g_loops = 0; // capacities
+    double *g_xc = nullptr;  // potID 3: x_cl and ddPot(x_cl) of every (step, site), 2 (N+2) loops
     double *g_xi = nullptr, *g_om = nullptr, *g_hist_buf = nullptr, *g_nfp = nullptr;
     uint32_t *g_w1 = nullptr, *g_w2 = nullptr;
     unsigned long long *g_seeds = nullptr;
@@ -626,12 +627,19 @@ int gs_reserve(sq_ctx *c) {
     if (c->g_lcg_scr == nullptr) SQ_HIP(hipMalloc(&c->g_lcg_scr, sizeof(unsigned long long) * sq::kLcgScratch));
     if (hist > c->g_hist) {
         (void)hipFree(c->g_hist_buf);
-        (void)hipFree(c->g_om);
-        c->g_hist_buf = c->g_om = nullptr;
+        c->g_hist_buf = nullptr;
         c->g_hist = 0;
         SQ_HIP(hipMalloc(&c->g_hist_buf, sizeof(double) * hist));
-        SQ_HIP(hipMalloc(&c->g_om, sizeof(double) * (c->p.loops + 1)));
         c->g_hist = hist;
+    }
+    if (c->p.loops > c->g_loops) {
+        (void)hipFree(c->g_om);
+        (void)hipFree(c->g_xc);
+        c->g_om = c->g_xc = nullptr;
+        c->g_loops = 0;
+        SQ_HIP(hipMalloc(&c->g_om, sizeof(double) * (c->p.loops + 1)));
+        SQ_HIP(hipMalloc(&c->g_xc, sizeof(double) * 2 * (c->N + 2) * (size_t)c->p.loops));
+        c->g_loops = c->p.loops;
     }
     if (!c->g_st) SQ_HIP(hipMalloc(&c->g_st, sizeof(sq::Qm1dGsState)));
     return SQ_OK;
@@ -664,6 +672,7 @@ int qm1d_gs_frame(sq_ctx *c, int *stable) {
     a.nfp = c->g_nfp;
     a.xi = c->g_xi;
     a.om = c->g_om;
+    a.xc = c->g_xc;
     a.hist = c->g_hist_buf;
     a.st = c->g_st;
     a.N = c->N;
@@ -898,7 +907,7 @@ int sq_destroy(sq_ctx *c) {
     }
     (void)hipFree(c->qst);
     for (double *q : c->qscr) (void)hipFree(q);
-    for (double *q : {c->g_xi, c->g_om, c->g_hist_buf, c->g_nfp}) (void)hipFree(q);
+    for (double *q : {c->g_xi, c->g_om, c->g_xc, c->g_hist_buf, c->g_nfp}) (void)hipFree(q);
     (void)hipFree(c->g_w1);
     (void)hipFree(c->g_w2);
     (void)hipFree(c->g_seeds);

@@ -99,6 +99,8 @@ struct Qm1dGsArgs {
     double *nfp;                   // the persistent newf buffer (never rolled back, tauhost.c)
     const double *xi;              // (N+1)*loops draws in call order
     double *om;                    // omega at the start of each step (loops+1)
+    double *xc;                    // potID 3: x_cl(i a, om[j]) at [j (N+2) + i + 1], i = -1..N,
+                                   // then ddPot of it at the same index + (N+2) loops
     double *hist;                  // field after each step (loops*N)
     Qm1dGsState *st;
     int N, pot, loops, runs;

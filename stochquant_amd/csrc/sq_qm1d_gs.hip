@@ -16,6 +16,9 @@
 //                    log/cos via fp64; glibc's logf/cosf round differently in
 //                    ~1% of arguments, so xi is within 1 ulp of the oracle's,
 //                    and bit-exact when the stream is injected).
+//   gs_omega_kernel  one wave: omega of every step (item N's scalar recurrence).
+//   gs_xcl_kernel    grid-wide, potID 3: x_cl and ddPot(x_cl) of every (step,
+//                    site), so the serial kernels below do no transcendentals.
 //   gs_sweep_kernel  one block (<= 16 waves): the GS field sweep as a skewed
 //                    pipeline.  Thread l owns sites [lB, lB+B) and runs step j
 //                    in phase p = l + j: the left neighbour's step-j value comes
@@ -295,180 +298,49 @@ __global__ __launch_bounds__(256) void gs_xi_kernel(const uint32_t *w1, const ui
     }
 }
 
-// -------------------------------------------------------------- sweep ----
-// Pipeline lane g (= thread index; W = blockDim/64 waves) runs step j in
-// phase g + j.  Inside a wave the neighbour values move by lane shuffles; the
-// two wave-edge values of a phase go through LDS, with one barrier after the
-// first site of the phase (right neighbour's step-(j-1) value) and one at its
-// end (left neighbour's step-j value).  CH sites per chunk; the noise of a
-// single-chunk phase is prefetched four phases ahead, of a multi-chunk phase
-// one chunk ahead.
-template <int CH>
-__global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int B, int om_lds) {
-    extern __shared__ double s_f[];  // the field, updated in place (the serial order's f)
-    double *s_om = s_f + A.N;        // om_lds: omega of every step, read once per phase
-    __shared__ double s_enew[16], s_eold[16], s_efirst[16];  // wave edges of the current phase
-    const int N = A.N, loops = A.loops, pot = A.pot;
-    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
-    const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
-    const int nl = (N + B - 1) / B;
-    const int i0 = g * B, i1 = min(N, i0 + B);
-    const bool owner = g < nl;
-
-    for (int i = g; i < N; i += blockDim.x) s_f[i] = A.f0[i];
-    if (wv == 0) {  // omega of every step: item N's update, :103-110,155-167.  64 draws
-       // per batch land in lanes; the (wave-uniform) recurrence reads them
-       // with readlane, and lane q keeps omega of step jb + q.
-        double w = A.st->omega_in;
-        const double top = (double)(N - 1) * a;
-        for (int jb = 0; jb < loops; jb += 64) {
-            const int nb = min(64, loops - jb);
-            const double dwl = lane < nb ? A.sigw * A.xi[(size_t)(jb + lane) * (N + 1) + N] : 0.;
-            double mine = 0.;
-            for (int q = 0; q < nb; ++q) {
-                if (lane == q) mine = w;
-                const double nw = w + A.kconst * __shfl(dwl, q, 64);
-                if (nw > top) w = 2 * (double)(N - 1) * a - nw;
-                else if (nw < 0) w = -nw;
-                else w = nw;
-            }
-            if (lane < nb) {
-                A.om[jb + lane] = mine;
-                if (om_lds) s_om[jb + lane] = mine;
-            }
+// -------------------------------------------------------- omega, x_cl ----
+// omega of every step: item N's update (:103-110,155-167), a scalar
+// recurrence.  64 draws per batch land in lanes; the wave-uniform recurrence
+// reads them with readlane, and lane q keeps omega of step jb + q.
+__global__ __launch_bounds__(64) void gs_omega_kernel(const Qm1dGsArgs A) {
+    const int N = A.N, loops = A.loops, lane = threadIdx.x;
+    const double a = A.a;
+    double w = A.st->omega_in;
+    const double top = (double)(N - 1) * a;
+    for (int jb = 0; jb < loops; jb += 64) {
+        const int nb = min(64, loops - jb);
+        const double dwl = lane < nb ? A.sigw * A.xi[(size_t)(jb + lane) * (N + 1) + N] : 0.;
+        const int dlo = __double2loint(dwl), dhi = __double2hiint(dwl);
+        double mine = 0.;
+        for (int q = 0; q < nb; ++q) {
+            if (lane == q) mine = w;
+            const double d = __hiloint2double(__builtin_amdgcn_readlane(dhi, q), __builtin_amdgcn_readlane(dlo, q));
+            const double nw = w + A.kconst * d;
+            if (nw > top) w = 2 * (double)(N - 1) * a - nw;
+            else if (nw < 0) w = -nw;
+            else w = nw;
         }
-        if (lane == 0) A.om[loops] = w;
+        if (lane < nb) A.om[jb + lane] = mine;
     }
-    __syncthreads();
+    if (lane == 0) A.om[loops] = w;
+}
 
-    double lastnew = 0., lastold = 0.;  // my block's last site after / before my current step
-    const int nchunk = (B + CH - 1) / CH;
-    auto load_chunk = [&](double (&dst)[CH], int j, int c) {
-#pragma unroll
-        for (int q = 0; q < CH; ++q) {
-            const int i = i0 + c * CH + q;
-            dst[q] = (owner && j >= 0 && j < loops && i < i1) ? A.xi[(size_t)j * (N + 1) + i] : 0.;
-        }
-    };
-    // state carried between the chunks of one phase
-    double prev_new = 0., prev_old = 0., firstval = 0., rfirst = 0.;
-    // sites c*CH .. c*CH+CH-1 of this lane's block at step j, noise in cur
-    auto run_chunk = [&](int j, int c, const double (&cur)[CH]) {
-        const bool act = owner && j >= 0 && j < loops;
-        const bool last = j == loops - 1;
-        const double w = act ? (om_lds ? s_om[j] : A.om[j]) : 0.;
-        // off the serial chain: old values, potential term, noise (same
-        // sub-expressions the chain below combines in the reference's order)
-        double fi[CH], rr[CH], t2[CH], dw[CH];
-#pragma unroll
-        for (int q = 0; q < CH; ++q) {
-            const int b = c * CH + q;
-            const int i = i0 + b;
-            fi[q] = (b < B && i < N) ? s_f[i] : 0.;
-            rr[q] = (b < B - 1 && i + 1 < N) ? s_f[i + 1] : 0.;  // right neighbour inside the block: old
-            t2[q] = ddpot(xcl((double)i * a, w, pot), pot) * fi[q] * h;
-            dw[q] = sig * cur[q];
-        }
-        const double xlo = xcl(-1. * a, w, pot), xhi = xcl((double)N * a, w, pot);
-#pragma unroll
-        for (int q = 0; q < CH; ++q) {
-            const int b = c * CH + q;
-            const int i = i0 + b;
-            const bool valid = act && i < i1;
-            if (b == B - 1) {  // lane g+1's first site, its step j-1 (computed at b = 0 of this phase)
-                rfirst = __shfl_down(firstval, 1, 64);
-                if (W > 1 && lane == 63 && wv < W - 1) rfirst = s_efirst[wv + 1];
-            }
-            if (b < B) {
-                double v = fi[q];
-                if (valid) {
-                    const double L = last ? prev_old : prev_new;
-                    double sum;
-                    if (i == 0) sum = rr[q] + (-kEta) - xlo - 2 * fi[q];  // N >= 2, B >= 2: rr = f[1]
-                    else if (i == N - 1) sum = L + kEta - xhi - 2 * fi[q];
-                    else sum = (b == B - 1 ? rfirst : rr[q]) + L - 2 * fi[q];
-                    v = fi[q] + kM * h * sum / a2 - t2[q] + dw[q];
-                    v = guard(v);
-                    A.hist[(size_t)j * N + i] = v;
-                    if (!last) s_f[i] = v;
-                }
-                prev_old = fi[q];
-                prev_new = v;
-                if (b == 0) firstval = v;  // = s_f[i0] after this phase's update (old value if idle)
-                if (i == i1 - 1) {
-                    lastnew = v;
-                    lastold = fi[q];
-                }
-            }
-            if (W > 1 && b == 0) {  // publish the wave's first value for the wave below
-                if (lane == 0) s_efirst[wv] = firstval;
-                __syncthreads();
-            }
-        }
-    };
-    auto begin_phase = [&]() {
-        prev_new = __shfl_up(lastnew, 1, 64);  // lane g-1's last site, its step j (previous phase)
-        prev_old = __shfl_up(lastold, 1, 64);
-        if (W > 1 && lane == 0 && wv > 0) {
-            prev_new = s_enew[wv - 1];
-            prev_old = s_eold[wv - 1];
-        }
-        firstval = rfirst = 0.;
-    };
-    auto end_phase = [&]() {  // publish the wave's last values for the next phase of the wave above
-        if (W > 1) {
-            if (lane == 63) {
-                s_enew[wv] = lastnew;
-                s_eold[wv] = lastold;
-            }
-            __syncthreads();
-        }
-    };
-    const int nphase = nl - 1 + loops;
-    if (nchunk == 1) {
-        // one chunk per phase: a phase is short, so the noise is prefetched
-        // four phases ahead through a four-slot register ring
-        double r0[CH], r1[CH], r2[CH], r3[CH];
-        load_chunk(r0, 0 - g, 0);
-        load_chunk(r1, 1 - g, 0);
-        load_chunk(r2, 2 - g, 0);
-        load_chunk(r3, 3 - g, 0);
-        auto phase = [&](int p, double (&slot)[CH]) {
-            begin_phase();
-            run_chunk(p - g, 0, slot);
-            load_chunk(slot, p + 4 - g, 0);
-            end_phase();
-        };
-        for (int p = 0; p < nphase; p += 4) {
-            phase(p, r0);
-            if (p + 1 >= nphase) break;
-            phase(p + 1, r1);
-            if (p + 2 >= nphase) break;
-            phase(p + 2, r2);
-            if (p + 3 >= nphase) break;
-            phase(p + 3, r3);
-        }
-    } else {
-        // several chunks per phase: the next chunk is prefetched while this one computes
-        double cur[CH], nxt[CH];
-        load_chunk(cur, -g, 0);
-        for (int p = 0; p < nphase; ++p) {
-            const int j = p - g;
-            begin_phase();
-            for (int c = 0; c < nchunk; ++c) {
-                if (c + 1 < nchunk) load_chunk(nxt, j, c + 1);
-                else load_chunk(nxt, j + 1, 0);
-                run_chunk(j, c, cur);
-#pragma unroll
-                for (int q = 0; q < CH; ++q) cur[q] = nxt[q];
-            }
-            end_phase();
-        }
+// potID 3: x_cl(i a, omega_j) for i = -1..N and ddPot of it, for every step
+// -- the only transcendental work of the sweep and the scan, hoisted off
+// their serial chains into one grid-wide pass.
+__global__ __launch_bounds__(256) void gs_xcl_kernel(const Qm1dGsArgs A) {
+    const int N = A.N, row = N + 2;
+    const long long n = (long long)row * A.loops;
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n;
+         k += (long long)gridDim.x * blockDim.x) {
+        const int j = (int)(k / row), i = (int)(k - (long long)j * row) - 1;
+        const double x = xcl(i == -1 ? -1. * A.a : (double)i * A.a, A.om[j], 3);
+        A.xc[k] = x;
+        A.xc[n + k] = ddpot(x, 3);
     }
 }
 
-// --------------------------------------------------------------- scan ----
-// ------------------------------------------------- scan, register path ----
+// ------------------------------------------------------------- DPP ----
 // Wave-wide max-scans by DPP (row_shr 1/2/4/8, row_bcast 15/31: the gfx9
 // inclusive-scan sequence), no LDS round trips; 64-bit values move as two
 // 32-bit DPP halves.  Out-of-range lanes read the identity (bound_ctrl off).
@@ -512,6 +384,144 @@ __device__ __forceinline__ int dpp_all_max_i(int v) {
 }
 __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
 
+// -------------------------------------------------------------- sweep ----
+// Pipeline lane g (= thread index; W = blockDim/64 waves) runs step j in
+// phase g + j.  Inside a wave the neighbour values move by lane shuffles; the
+// two wave-edge values of a phase go through LDS, with one barrier after the
+// first site of the phase (right neighbour's step-(j-1) value) and one at its
+// end (left neighbour's step-j value).  B <= CH sites per lane, held in
+// registers; the noise is prefetched a few phases ahead.
+template <int CH>
+struct GsChunk {
+    double x[CH], d[CH];  // noise, ddPot(x_cl) per site
+    double lo, hi;        // x_cl at sites -1 and N (the boundary terms)
+};
+
+template <int CH, bool P3>
+__global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int B) {
+    __shared__ double s_enew[16], s_eold[16], s_efirst[16];  // wave edges of the current phase
+    const int N = A.N, loops = A.loops, pot = A.pot;
+    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
+    const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
+    const int nl = (N + B - 1) / B;
+    const int i0 = g * B, i1 = min(N, i0 + B);
+    const bool owner = g < nl;
+
+    // my sites' field (the serial order's f; only the owner lane reads or writes them)
+    double f_[CH];
+#pragma unroll
+    for (int q = 0; q < CH; ++q) f_[q] = (owner && q < B && i0 + q < N) ? A.f0[i0 + q] : 0.;
+
+    double lastnew = 0., lastold = 0.;  // my block's last site after / before my current step
+    constexpr bool p3 = P3;  // potID 3 (x_cl terms), else ddPot = 2 and x_cl = 0
+    const size_t dd_off = (size_t)(N + 2) * loops;
+    // noise (and for potID 3 ddPot(x_cl) and the boundary x_cl) of one chunk
+    auto load_chunk = [&](GsChunk<CH> &dst, int j) {
+        const bool act = owner && j >= 0 && j < loops;
+        const double *xr = A.xi + (size_t)j * (N + 1);
+        const double *cr = A.xc + (size_t)j * (N + 2);
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const int i = i0 + q;
+            dst.x[q] = (act && i < i1) ? xr[i] : 0.;
+            dst.d[q] = (p3 && act && i < i1) ? cr[dd_off + i + 1] : 2.;
+        }
+        dst.lo = (p3 && act && i0 == 0) ? cr[0] : 0.;
+        dst.hi = (p3 && act && i1 == N) ? cr[N + 1] : 0.;
+    };
+    // state carried through one phase
+    double prev_new = 0., prev_old = 0., firstval = 0., rfirst = 0.;
+    // this lane's sites at step j, noise in cur
+    auto run_chunk = [&](int j, const GsChunk<CH> &cur) {
+        const bool act = owner && j >= 0 && j < loops;
+        const bool last = j == loops - 1;
+        // off the serial chain: old values, potential term, noise (same
+        // sub-expressions the chain below combines in the reference's order)
+        double fi[CH], rr[CH], t2[CH], dw[CH];
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const int b = q;
+            fi[q] = f_[q];
+            rr[q] = q + 1 < CH && b < B - 1 ? f_[q + 1] : 0.;  // right neighbour inside the block: old
+            t2[q] = cur.d[q] * fi[q] * h;  // ddPot(x_cl) * f * h; ddPot = 2 off potID 3
+            dw[q] = sig * cur.x[q];
+        }
+        const double xlo = cur.lo, xhi = cur.hi;
+#pragma unroll
+        for (int q = 0; q < CH; ++q) {
+            const int b = q;
+            const int i = i0 + b;
+            const bool valid = act && i < i1;
+            if (b == B - 1) {  // lane g+1's first site, its step j-1 (computed at b = 0 of this phase)
+                rfirst = dpp_d<0x130, 0xf, 0xf>(firstval, 0.);  // wave_shl:1
+                if (W > 1 && lane == 63 && wv < W - 1) rfirst = s_efirst[wv + 1];
+            }
+            if (b < B) {
+                double v = fi[q];
+                if (valid) {
+                    const double L = last ? prev_old : prev_new;
+                    double sum;
+                    if (i == 0) sum = rr[q] + (-kEta) - xlo - 2 * fi[q];  // N >= 2, B >= 2: rr = f[1]
+                    else if (i == N - 1) sum = L + kEta - xhi - 2 * fi[q];
+                    else sum = (b == B - 1 ? rfirst : rr[q]) + L - 2 * fi[q];
+                    v = fi[q] + kM * h * sum / a2 - t2[q] + dw[q];
+                    v = guard(v);
+                    A.hist[(size_t)j * N + i] = v;
+                    if (!last) f_[q] = v;
+                }
+                prev_old = fi[q];
+                prev_new = v;
+                if (b == 0) firstval = v;  // = f[i0] after this phase's update (old value if idle)
+                if (i == i1 - 1) {
+                    lastnew = v;
+                    lastold = fi[q];
+                }
+            }
+            if (W > 1 && b == 0) {  // publish the wave's first value for the wave below
+                if (lane == 0) s_efirst[wv] = firstval;
+                __syncthreads();
+            }
+        }
+    };
+    auto begin_phase = [&]() {
+        prev_new = dpp_d<0x138, 0xf, 0xf>(lastnew, 0.);  // wave_shr:1: lane g-1's last site, its step j
+        prev_old = dpp_d<0x138, 0xf, 0xf>(lastold, 0.);  // (previous phase)
+        if (W > 1 && lane == 0 && wv > 0) {
+            prev_new = s_enew[wv - 1];
+            prev_old = s_eold[wv - 1];
+        }
+        firstval = rfirst = 0.;
+    };
+    auto end_phase = [&]() {  // publish the wave's last values for the next phase of the wave above
+        if (W > 1) {
+            if (lane == 63) {
+                s_enew[wv] = lastnew;
+                s_eold[wv] = lastold;
+            }
+            __syncthreads();
+        }
+    };
+    const int nphase = nl - 1 + loops;
+    // one chunk per phase (B <= CH): a phase is short, so the noise is
+    // prefetched RD phases ahead through a register ring
+    constexpr int RD = CH == 2 && !P3 ? 4 : CH == 2 ? 3 : 2;
+    GsChunk<CH> ring[RD];
+#pragma unroll
+    for (int r = 0; r < RD; ++r) load_chunk(ring[r], r - g);
+    for (int p = 0; p < nphase; p += RD) {
+#pragma unroll
+        for (int r = 0; r < RD; ++r) {
+            if (p + r >= nphase) break;
+            begin_phase();
+            run_chunk(p + r - g, ring[r]);
+            load_chunk(ring[r], p + r + RD - g);
+            end_phase();
+        }
+    }
+}
+
+// --------------------------------------------------------------- scan ----
+
 // N <= 64 KB: the lane's KB sites stay in registers (field, running means,
 // this step's X, |X|, drift check), the next step's inputs are prefetched, and
 // only f / nf go through LDS for the cross-lane reads of nf[E] and f[mid].
@@ -526,7 +536,7 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
     const int i0 = lane * B, i1 = min(N, i0 + B);
     const double a = A.a, sig = A.sig;
     const double NEG = -__builtin_inf();
-    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB];
+    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB], pc[KB];
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
         const int i = i0 + b;
@@ -536,15 +546,18 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
         xx_[b] = in ? A.xx00[i] : 0.;
         if (in) s_f[i] = f_[b];
     }
+    const bool p3 = pot == 3;
     auto prefetch = [&](int j) {
         const double *row = A.hist + (size_t)j * N;
         const double *xr = A.xi + (size_t)j * (N + 1);
+        const double *cr = A.xc + (size_t)j * (N + 2) + 1;
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
             const int i = i0 + b;
             const bool in = b < B && i < i1;
             pr[b] = in ? row[i] : 0.;
             px[b] = in ? xr[i] : 0.;
+            pc[b] = (p3 && in) ? cr[i] : 0.;
         }
     };
     prefetch(0);
@@ -552,17 +565,15 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
     int E = A.st->lrgEl;
     double V = A.st->lrgVl;
     int brk_step = -1, brk_item = -1;
-    double w_next = A.om[0];
     double n[KB];
     for (int j = 0; j < loops; ++j) {
-        const double w = w_next;
-        if (j + 1 < loops) w_next = A.om[j + 1];
+        const double *crow = A.xc + (size_t)j * (N + 2) + 1;  // x_cl of this step (potID 3)
         double X[KB], D[KB], xc[KB];
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
             const int i = i0 + b;
             n[b] = pr[b];
-            xc[b] = xcl((double)i * a, w, pot);
+            xc[b] = pc[b];
             X[b] = n[b] + xc[b];
             D[b] = absol(n[b] - f_[b] - sig * px[b]);  // :139, |nf - f - dw|
             if (b < B && i < i1) s_n[i] = n[b];
@@ -571,7 +582,7 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
         // nf[E] before item E runs this step: the previous step's value
         // (the persistent newf buffer at j = 0)
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
-        const double T0 = nfE + xcl((double)E * a, w, pot);
+        const double T0 = nfE + (p3 ? crow[E] : 0.);
         double m1 = NEG, ty = NEG, ta = NEG;
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
@@ -627,7 +638,7 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
         }
         __syncthreads();  // s_n of every lane written (f[mid] new)
         const double den = (double)(A.runs + j + 1);
-        const double xm = xcl((double)mid * a, w, pot);
+        const double xm = p3 ? crow[mid] : 0.;
         const double fm_old = s_f[mid], fm_new = s_n[mid];
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
@@ -688,7 +699,7 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
     const int i0 = g * B, i1 = min(N, i0 + B);
     const double a = A.a, sig = A.sig;
     const double NEG = -__builtin_inf();
-    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB];
+    double f_[KB], x_[KB], xx_[KB], pr[KB], px[KB], pc[KB];
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
         const int i = i0 + b;
@@ -698,15 +709,18 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
         xx_[b] = in ? A.xx00[i] : 0.;
         if (in) s_f[i] = f_[b];
     }
+    const bool p3 = pot == 3;
     auto prefetch = [&](int j) {
         const double *row = A.hist + (size_t)j * N;
         const double *xr = A.xi + (size_t)j * (N + 1);
+        const double *cr = A.xc + (size_t)j * (N + 2) + 1;
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
             const int i = i0 + b;
             const bool in = b < B && i < i1;
             pr[b] = in ? row[i] : 0.;
             px[b] = in ? xr[i] : 0.;
+            pc[b] = (p3 && in) ? cr[i] : 0.;
         }
     };
     prefetch(0);
@@ -714,18 +728,16 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
     int E = A.st->lrgEl;
     double V = A.st->lrgVl;
     int brk_step = -1, brk_item = -1;
-    double w_next = A.om[0];
     double n[KB];
     for (int j = 0; j < loops; ++j) {
-        const double w = w_next;
-        if (j + 1 < loops) w_next = A.om[j + 1];
+        const double *crow = A.xc + (size_t)j * (N + 2) + 1;  // x_cl of this step (potID 3)
         double X[KB], D[KB], xc[KB];
         double m1 = NEG, ta = NEG;
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
             const int i = i0 + b;
             n[b] = pr[b];
-            xc[b] = xcl((double)i * a, w, pot);
+            xc[b] = pc[b];
             X[b] = n[b] + xc[b];
             D[b] = absol(n[b] - f_[b] - sig * px[b]);  // :139, |nf - f - dw|
             if (b < B && i < i1) {
@@ -745,7 +757,7 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
         }
         __syncthreads();  // #1: s_n, wave maxima of X below E and of |X|
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
-        const double T0 = nfE + xcl((double)E * a, w, pot);
+        const double T0 = nfE + (p3 ? crow[E] : 0.);
         // lane k reads wave k's partial: one LDS load and a DPP reduction per quantity
         const double M1 = dpp_all_max(lane < W ? s_m1[lane] : NEG);
         const double ta_all = dpp_all_max(lane < W ? s_ta[lane] : NEG);
@@ -813,7 +825,7 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
             break;
         }
         const double den = (double)(A.runs + j + 1);
-        const double xm = xcl((double)mid * a, w, pot);
+        const double xm = p3 ? crow[mid] : 0.;
         const double fm_old = s_f[mid], fm_new = s_n[mid];
 #pragma unroll
         for (int b = 0; b < KB; ++b) {
@@ -859,8 +871,6 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
 
 }  // namespace
 
-constexpr int kSweepLdsMax = 96 * 1024;
-
 int qm1d_gs_block(int N) {  // sites per pipeline lane: 2 while <= 1024 lanes (16 waves) suffice
     if (N < 2 || N > kQm1dGsMaxN) return 0;
     return std::max(2, (N + 1023) / 1024);
@@ -889,6 +899,12 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const int B = qm1d_gs_block(a.N);
     if (B == 0) return hipErrorInvalidValue;
     const size_t lds1 = sizeof(double) * (size_t)a.N;
+    hipLaunchKernelGGL(gs_omega_kernel, dim3(1), dim3(64), 0, s, a);
+    if (a.pot == 3) {
+        const long long n = (long long)(a.N + 2) * a.loops;
+        const int blocks = (int)std::min<long long>(2048, (n + 255) / 256);
+        hipLaunchKernelGGL(gs_xcl_kernel, dim3(blocks), dim3(256), 0, s, a);
+    }
     // the dynamic-LDS limit is a per-device function attribute: set it once per device
     static bool attr_set[64] = {};
     int dev = 0;
@@ -899,20 +915,15 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
         if ((e = hipFuncSetAttribute((const void *)gs_scan_mw_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)(2 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
             return e;
-        for (const void *k : {(const void *)gs_sweep_kernel<2>, (const void *)gs_sweep_kernel<8>})
-            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, kSweepLdsMax)) != hipSuccess)
-                return e;
         attr = true;
     }
-    // omega of all steps next to the field in LDS when it fits (one LDS read per phase
-    // instead of a global load on the pipeline's critical path)
-    const size_t lds_om = sizeof(double) * ((size_t)a.N + a.loops + 1);
-    const int om_lds = lds_om <= (size_t)kSweepLdsMax ? 1 : 0;
-    const size_t lds_sw = om_lds ? lds_om : lds1;
     const int nl = (a.N + B - 1) / B;
     const int threads = 64 * ((nl + 63) / 64);  // one pipeline lane per thread, <= 1024
-    if (B <= 2) hipLaunchKernelGGL(gs_sweep_kernel<2>, dim3(1), dim3(threads), lds_sw, s, a, B, om_lds);
-    else hipLaunchKernelGGL(gs_sweep_kernel<8>, dim3(1), dim3(threads), lds_sw, s, a, B, om_lds);
+    const bool p3 = a.pot == 3;
+    if (B <= 2 && p3) hipLaunchKernelGGL((gs_sweep_kernel<2, true>), dim3(1), dim3(threads), 0, s, a, B);
+    else if (B <= 2) hipLaunchKernelGGL((gs_sweep_kernel<2, false>), dim3(1), dim3(threads), 0, s, a, B);
+    else if (p3) hipLaunchKernelGGL((gs_sweep_kernel<4, true>), dim3(1), dim3(threads), 0, s, a, B);
+    else hipLaunchKernelGGL((gs_sweep_kernel<4, false>), dim3(1), dim3(threads), 0, s, a, B);
     const size_t lds2 = 2 * lds1;
     if (a.N <= 128) {
         hipLaunchKernelGGL(gs_scan_reg_kernel<2>, dim3(1), dim3(64), lds2, s, a);
