@@ -695,6 +695,7 @@ int qm1d_gs_frame(sq_ctx *c, int *stable) {
     if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
     SQ_HIP(hipMemcpyAsync(&st, c->g_st, sizeof st, hipMemcpyDeviceToHost, c->qstream));
     SQ_HIP(hipStreamSynchronize(c->qstream));
+    if (st.sync_error) return fail(SQ_E_HIP, "serial frame: the scan timed out waiting for the sweep");
     c->consumed = (unsigned long long)st.consumed;
     if (!injected && st.consumed > 0)
         SQ_HIP(hipMemcpy(&c->lcg_seed, c->g_seeds + (st.consumed - 1), sizeof(unsigned long long),

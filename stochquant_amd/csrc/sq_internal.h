@@ -89,8 +89,10 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
 // QM1D in the reference's serial order (sq_qm1d_gs.hip)
 struct Qm1dGsState {
     double omega_in, omega_out, lrgVl;
-    int lrgEl, stable, steps_done, pad;
+    int lrgEl, stable, steps_done;
+    int rows_ready;      // steps the sweep has completed (sweep -> scan handshake; 0 at upload)
     long long consumed;  // random() calls the launch made (the shared seed advances by these)
+    int sync_error, pad; // the scan timed out waiting for the sweep
 };
 
 struct Qm1dGsArgs {

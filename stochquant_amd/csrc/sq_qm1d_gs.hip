@@ -384,6 +384,35 @@ __device__ __forceinline__ int dpp_all_max_i(int v) {
 }
 __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
 
+// ---------------------------------------------------- sweep -> scan ----
+// The sweep and the scan of a frame run concurrently, as two blocks of one
+// launch: the sweep publishes how many steps (rows of hist) are complete,
+// the scan waits for the rows it is about to read.  Release/acquire at agent
+// scope (the blocks sit on different XCDs, each with its own L2).
+constexpr int kPublishEvery = 32;  // phases between two sweep publications
+
+__device__ __forceinline__ void gs_publish_rows(const Qm1dGsArgs &A, int rows, int W) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's hist stores
+    if (W > 1) __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&A.st->rows_ready, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wait until `need` rows are complete (avail caches the last value seen).
+// False after ~2 s without progress: the frame reports an error instead of
+// spinning forever.
+__device__ __forceinline__ bool gs_wait_rows(const Qm1dGsArgs &A, int need, int &avail) {
+    if (need <= avail) return true;
+    int p;
+    long long spins = 0;
+    while ((p = __hip_atomic_load(&A.st->rows_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < need) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1ll << 25)) return false;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    avail = p;
+    return true;
+}
+
 // -------------------------------------------------------------- sweep ----
 // Pipeline lane g (= thread index; W = blockDim/64 waves) runs step j in
 // phase g + j.  Inside a wave the neighbour values move by lane shuffles; the
@@ -398,10 +427,10 @@ struct GsChunk {
 };
 
 template <int CH, bool P3>
-__global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int B) {
+__device__ __forceinline__ void gs_sweep(const Qm1dGsArgs &A, int B, int nthreads) {
     __shared__ double s_enew[16], s_eold[16], s_efirst[16];  // wave edges of the current phase
     const int N = A.N, loops = A.loops, pot = A.pot;
-    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
+    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = nthreads >> 6;
     const double h = A.h, a = A.a, a2 = A.a2, sig = A.sig;
     const int nl = (N + B - 1) / B;
     const int i0 = g * B, i1 = min(N, i0 + B);
@@ -516,6 +545,8 @@ __global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int 
             run_chunk(p + r - g, ring[r]);
             load_chunk(ring[r], p + r + RD - g);
             end_phase();
+            const int q = p + r + 1;  // phases done; step j is complete after phase nl-1+j
+            if (q % kPublishEvery == 0 || q == nphase) gs_publish_rows(A, min(loops, max(0, q - nl + 1)), W);
         }
     }
 }
@@ -527,8 +558,7 @@ __global__ __launch_bounds__(1024) void gs_sweep_kernel(const Qm1dGsArgs A, int 
 // only f / nf go through LDS for the cross-lane reads of nf[E] and f[mid].
 // The stability scan of one step as prefix maxima.
 template <int KB>
-__global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
-    extern __shared__ double lds[];
+__device__ __forceinline__ void gs_scan_reg(const Qm1dGsArgs &A, double *lds) {
     const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
     double *s_f = lds, *s_n = lds + N;
     const int lane = threadIdx.x;
@@ -560,6 +590,11 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
             pc[b] = (p3 && in) ? cr[i] : 0.;
         }
     };
+    int avail = 0;
+    if (!gs_wait_rows(A, 1, avail)) {
+        if (threadIdx.x == 0) A.st->sync_error = 1;
+        return;
+    }
     prefetch(0);
     __syncthreads();
     int E = A.st->lrgEl;
@@ -578,7 +613,13 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
             D[b] = absol(n[b] - f_[b] - sig * px[b]);  // :139, |nf - f - dw|
             if (b < B && i < i1) s_n[i] = n[b];
         }
-        if (j + 1 < loops) prefetch(j + 1);
+        if (j + 1 < loops) {
+            if (!gs_wait_rows(A, j + 2, avail)) {
+                if (threadIdx.x == 0) A.st->sync_error = 1;
+                return;
+            }
+            prefetch(j + 1);
+        }
         // nf[E] before item E runs this step: the previous step's value
         // (the persistent newf buffer at j = 0)
         const double nfE = j == 0 ? A.nfp[E] : s_f[E];
@@ -688,14 +729,13 @@ __global__ __launch_bounds__(64) void gs_scan_reg_kernel(const Qm1dGsArgs A) {
 // DPP scans are joined across waves through LDS (four barriers per step).
 // Same semantics and expression order as gs_scan_reg_kernel.
 template <int KB>
-__global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
-    extern __shared__ double lds[];
+__device__ __forceinline__ void gs_scan_mw(const Qm1dGsArgs &A, double *lds, int nthreads) {
     __shared__ double s_m1[16], s_ta[16], s_ty[16], s_vbad;
     __shared__ int s_fb[16], s_ll[16];
     const int N = A.N, loops = A.loops, pot = A.pot, mid = N / 2;
     double *s_f = lds, *s_n = lds + N;
-    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = blockDim.x >> 6;
-    const int B = (N + blockDim.x - 1) / blockDim.x;
+    const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = nthreads >> 6;
+    const int B = (N + nthreads - 1) / nthreads;
     const int i0 = g * B, i1 = min(N, i0 + B);
     const double a = A.a, sig = A.sig;
     const double NEG = -__builtin_inf();
@@ -723,6 +763,11 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
             pc[b] = (p3 && in) ? cr[i] : 0.;
         }
     };
+    int avail = 0;
+    if (!gs_wait_rows(A, 1, avail)) {
+        if (threadIdx.x == 0) A.st->sync_error = 1;
+        return;
+    }
     prefetch(0);
     __syncthreads();
     int E = A.st->lrgEl;
@@ -746,7 +791,13 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
                 ta = fmax(ta, absol(X[b]));
             }
         }
-        if (j + 1 < loops) prefetch(j + 1);
+        if (j + 1 < loops) {
+            if (!gs_wait_rows(A, j + 2, avail)) {
+                if (threadIdx.x == 0) A.st->sync_error = 1;
+                return;
+            }
+            prefetch(j + 1);
+        }
         const double ta_wex = dpp_excl_max(ta);
         {
             const double m1w = dpp_all_max(m1), taw = dpp_all_max(ta);
@@ -869,6 +920,22 @@ __global__ __launch_bounds__(1024) void gs_scan_mw_kernel(const Qm1dGsArgs A) {
     }
 }
 
+// One frame's sweep (block 0) and scan (block 1), concurrently.  Waves past
+// a block's own thread count exit at once.  SC: scan variant (0: one wave,
+// 2 sites per lane; 1: one wave, 4; 2: multi-wave).
+template <int CH, bool P3, int SC>
+__global__ __launch_bounds__(SC == 2 ? 1024 : 256) void gs_frame_kernel(const Qm1dGsArgs A, int B, int sweep_threads,
+                                                                        int scan_threads) {
+    extern __shared__ double lds[];
+    if (blockIdx.x == 0) {
+        if ((int)threadIdx.x < sweep_threads) gs_sweep<CH, P3>(A, B, sweep_threads);
+    } else if ((int)threadIdx.x < scan_threads) {
+        if constexpr (SC == 0) gs_scan_reg<2>(A, lds);
+        else if constexpr (SC == 1) gs_scan_reg<4>(A, lds);
+        else gs_scan_mw<4>(A, lds, scan_threads);
+    }
+}
+
 }  // namespace
 
 int qm1d_gs_block(int N) {  // sites per pipeline lane: 2 while <= 1024 lanes (16 waves) suffice
@@ -912,27 +979,31 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     bool &attr = attr_set[dev];
     if (!attr) {
         hipError_t e;
-        if ((e = hipFuncSetAttribute((const void *)gs_scan_mw_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)(2 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
-            return e;
+        for (const void *k : {(const void *)gs_frame_kernel<2, false, 0>, (const void *)gs_frame_kernel<2, true, 0>,
+                              (const void *)gs_frame_kernel<2, false, 1>, (const void *)gs_frame_kernel<2, true, 1>,
+                              (const void *)gs_frame_kernel<2, false, 2>, (const void *)gs_frame_kernel<2, true, 2>,
+                              (const void *)gs_frame_kernel<4, false, 2>, (const void *)gs_frame_kernel<4, true, 2>})
+            if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(2 * sizeof(double) * kQm1dGsMaxN))) != hipSuccess)
+                return e;
         attr = true;
     }
     const int nl = (a.N + B - 1) / B;
-    const int threads = 64 * ((nl + 63) / 64);  // one pipeline lane per thread, <= 1024
-    const bool p3 = a.pot == 3;
-    if (B <= 2 && p3) hipLaunchKernelGGL((gs_sweep_kernel<2, true>), dim3(1), dim3(threads), 0, s, a, B);
-    else if (B <= 2) hipLaunchKernelGGL((gs_sweep_kernel<2, false>), dim3(1), dim3(threads), 0, s, a, B);
-    else if (p3) hipLaunchKernelGGL((gs_sweep_kernel<4, true>), dim3(1), dim3(threads), 0, s, a, B);
-    else hipLaunchKernelGGL((gs_sweep_kernel<4, false>), dim3(1), dim3(threads), 0, s, a, B);
+    const int sweep_threads = 64 * ((nl + 63) / 64);  // one pipeline lane per thread, <= 1024
+    // scan: one wave up to 256 sites (measured faster than two waves with barriers),
+    // else 2 sites per thread up to 2048 sites (16 waves), up to 4 beyond
+    const int scan_threads = a.N <= 256 ? 64 : 64 * std::min(16, (a.N + 127) / 128);
+    const dim3 grid(2), block(std::max(sweep_threads, scan_threads));
     const size_t lds2 = 2 * lds1;
-    if (a.N <= 128) {
-        hipLaunchKernelGGL(gs_scan_reg_kernel<2>, dim3(1), dim3(64), lds2, s, a);
-    } else if (a.N <= 256) {  // one wave without barriers still beats two waves here (measured)
-        hipLaunchKernelGGL(gs_scan_reg_kernel<4>, dim3(1), dim3(64), lds2, s, a);
-    } else {  // 2 sites per thread up to 2048 sites (16 waves), up to 4 beyond
-        const int waves = std::min(16, (a.N + 127) / 128);
-        hipLaunchKernelGGL(gs_scan_mw_kernel<4>, dim3(1), dim3(64 * waves), lds2, s, a);
-    }
+    const bool p3 = a.pot == 3;
+#define SQ_GS_FRAME(CH, SC)                                                                                     \
+    hipLaunchKernelGGL((p3 ? gs_frame_kernel<CH, true, SC> : gs_frame_kernel<CH, false, SC>), grid, block, lds2, \
+                       s, a, B, sweep_threads, scan_threads)
+    if (a.N <= 128) SQ_GS_FRAME(2, 0);
+    else if (a.N <= 256) SQ_GS_FRAME(2, 1);
+    else if (B <= 2) SQ_GS_FRAME(2, 2);
+    else SQ_GS_FRAME(4, 2);
+#undef SQ_GS_FRAME
     return hipGetLastError();
 }
 
