@@ -3,14 +3,14 @@
 // running means exactly as time_dev runs when its work-items execute in id
 // order between barriers (oracle/orc_qm1d.c serial).
 //
-// Four launches per frame, all on one stream:
-//   gs_lcg_kernel    one block: the LCG of tau_kernel.cl:269-284 for every
-//                    call of a full launch (rounds 0..loops-1, items 0..N),
-//                    incl. the isinf retry; stores the accepted draw's words
-//                    t1>>16, t2>>16 and the seed after each call.  The seed
-//                    update is affine mod 2^48 except on rare calls, so the
-//                    serial chain is a parallel prefix of affine maps plus an
-//                    exact serial fix-up at the exceptions (see below).
+// Launches per frame, all on one stream:
+//   gs_lcg_*_kernel  the LCG of tau_kernel.cl:269-284 for every call of a
+//                    full launch (rounds 0..loops-1, items 0..N), incl. the
+//                    isinf retry; stores the accepted draw's words t1>>16,
+//                    t2>>16 and the seed after each call.  The seed update is
+//                    affine mod 2^48 except on rare calls, so the serial chain
+//                    is a parallel prefix of affine maps (grid-wide) plus an
+//                    exact one-block fix-up from the first exception (below).
 //   gs_xi_kernel     grid-wide: xi = cos(2*3.1415*v2) * sqrt(-2 log v1) with
 //                    the reference's float casts (correctly rounded float
 //                    log/cos via fp64; glibc's logf/cosf round differently in
@@ -19,23 +19,25 @@
 //   gs_omega_kernel  one wave: omega of every step (item N's scalar recurrence).
 //   gs_xcl_kernel    grid-wide, potID 3: x_cl and ddPot(x_cl) of every (step,
 //                    site), so the serial kernels below do no transcendentals.
-//   gs_sweep_kernel  one block (<= 16 waves): the GS field sweep as a skewed
+//   gs_frame_kernel  two blocks running concurrently:
+//     block 0, the sweep (<= 16 waves): the GS field sweep as a skewed
 //                    pipeline.  Thread l owns sites [lB, lB+B) and runs step j
-//                    in phase p = l + j: the left neighbour's step-j value comes
-//                    from thread l-1's previous phase, the right neighbour's
-//                    step-(j-1) value from thread l+1's first site of the same
-//                    phase (lane shuffles inside a wave, LDS across waves).  Every
-//                    (step, site) is computed exactly as the serial order
-//                    computes it, with the reference's expression order.  The
-//                    field of every step goes to hist (loops x N).
-//   gs_scan_*_kernel one block: walks the steps in order and evaluates the
-//                    stability scan (tau_kernel.cl:135-143) as prefix maxima
-//                    (derivation in DESIGN.md §QM1D serial mode), finds the
-//                    first unstable item (the serial break: items after it
-//                    never run that round -- except in round 0, where the
-//                    stable test has not started, :168-171) and the running
-//                    means :144-145.
+//                    in phase p = l + j: the left neighbour's step-j value
+//                    comes from thread l-1's previous phase, the right
+//                    neighbour's step-(j-1) value from thread l+1's first site
+//                    of the same phase (DPP wave shifts inside a wave, LDS
+//                    across waves).  Every (step, site) is computed exactly as
+//                    the serial order computes it, with the reference's
+//                    expression order.  The field of every step goes to hist
+//                    (loops x N); completed steps are published to the scan.
+//     block 1, the scan: walks the steps as their rows appear and evaluates
+//                    the stability scan (tau_kernel.cl:135-143) as prefix
+//                    maxima (derivation in DESIGN.md §4.1), finds the first
+//                    unstable item (the serial break: items after it never run
+//                    that round -- except in round 0, where the stable test has
+//                    not started, :168-171) and the running means :144-145.
 #include <algorithm>
+#include <cstdlib>
 
 #include "sq_internal.h"
 
@@ -389,7 +391,7 @@ __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v);
 // launch: the sweep publishes how many steps (rows of hist) are complete,
 // the scan waits for the rows it is about to read.  Release/acquire at agent
 // scope (the blocks sit on different XCDs, each with its own L2).
-constexpr int kPublishEvery = 32;  // phases between two sweep publications
+constexpr int kPublishEvery = 32;  // default phases between two sweep publications
 
 __device__ __forceinline__ void gs_publish_rows(const Qm1dGsArgs &A, int rows, int W) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // this wave's hist stores
@@ -427,7 +429,7 @@ struct GsChunk {
 };
 
 template <int CH, bool P3>
-__device__ __forceinline__ void gs_sweep(const Qm1dGsArgs &A, int B, int nthreads) {
+__device__ __forceinline__ void gs_sweep(const Qm1dGsArgs &A, int B, int nthreads, int publish) {
     __shared__ double s_enew[16], s_eold[16], s_efirst[16];  // wave edges of the current phase
     const int N = A.N, loops = A.loops, pot = A.pot;
     const int g = threadIdx.x, lane = g & 63, wv = g >> 6, W = nthreads >> 6;
@@ -546,7 +548,7 @@ __device__ __forceinline__ void gs_sweep(const Qm1dGsArgs &A, int B, int nthread
             load_chunk(ring[r], p + r + RD - g);
             end_phase();
             const int q = p + r + 1;  // phases done; step j is complete after phase nl-1+j
-            if (q % kPublishEvery == 0 || q == nphase) gs_publish_rows(A, min(loops, max(0, q - nl + 1)), W);
+            if (q % publish == 0 || q == nphase) gs_publish_rows(A, min(loops, max(0, q - nl + 1)), W);
         }
     }
 }
@@ -925,10 +927,10 @@ __device__ __forceinline__ void gs_scan_mw(const Qm1dGsArgs &A, double *lds, int
 // 2 sites per lane; 1: one wave, 4; 2: multi-wave).
 template <int CH, bool P3, int SC>
 __global__ __launch_bounds__(SC == 2 ? 1024 : 256) void gs_frame_kernel(const Qm1dGsArgs A, int B, int sweep_threads,
-                                                                        int scan_threads) {
+                                                                        int scan_threads, int publish) {
     extern __shared__ double lds[];
     if (blockIdx.x == 0) {
-        if ((int)threadIdx.x < sweep_threads) gs_sweep<CH, P3>(A, B, sweep_threads);
+        if ((int)threadIdx.x < sweep_threads) gs_sweep<CH, P3>(A, B, sweep_threads, publish);
     } else if ((int)threadIdx.x < scan_threads) {
         if constexpr (SC == 0) gs_scan_reg<2>(A, lds);
         else if constexpr (SC == 1) gs_scan_reg<4>(A, lds);
@@ -996,9 +998,14 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const dim3 grid(2), block(std::max(sweep_threads, scan_threads));
     const size_t lds2 = 2 * lds1;
     const bool p3 = a.pot == 3;
+    static const int publish = [] {
+        const char *e = getenv("SQ_GS_PUBLISH");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 ? v : kPublishEvery;
+    }();
 #define SQ_GS_FRAME(CH, SC)                                                                                     \
     hipLaunchKernelGGL((p3 ? gs_frame_kernel<CH, true, SC> : gs_frame_kernel<CH, false, SC>), grid, block, lds2, \
-                       s, a, B, sweep_threads, scan_threads)
+                       s, a, B, sweep_threads, scan_threads, publish)
     if (a.N <= 128) SQ_GS_FRAME(2, 0);
     else if (a.N <= 256) SQ_GS_FRAME(2, 1);
     else if (B <= 2) SQ_GS_FRAME(2, 2);
