@@ -108,6 +108,9 @@ struct sq_ctx {
     unsigned long long consumed = 0;   // random() calls of the last serial frame
     long long g_calls = 0, g_hist = 0, g_loops = 0; // capacities
     double *g_xc = nullptr;  // potID 3: x_cl and ddPot(x_cl) of every (step, site), 2 (N+2) loops
+    void *g_cand = nullptr;  // serial scan candidates per step
+    int *g_flags = nullptr;  // per-step "candidates ready" flags, compared with gs_tag
+    int gs_tag = 0;
     double *g_xi = nullptr, *g_om = nullptr, *g_hist_buf = nullptr, *g_nfp = nullptr;
     uint32_t *g_w1 = nullptr, *g_w2 = nullptr;
     unsigned long long *g_seeds = nullptr;
@@ -635,10 +638,18 @@ int gs_reserve(sq_ctx *c) {
     if (c->p.loops > c->g_loops) {
         (void)hipFree(c->g_om);
         (void)hipFree(c->g_xc);
+        (void)hipFree(c->g_cand);
+        (void)hipFree(c->g_flags);
         c->g_om = c->g_xc = nullptr;
+        c->g_cand = nullptr;
+        c->g_flags = nullptr;
         c->g_loops = 0;
         SQ_HIP(hipMalloc(&c->g_om, sizeof(double) * (c->p.loops + 1)));
         SQ_HIP(hipMalloc(&c->g_xc, sizeof(double) * 2 * (c->N + 2) * (size_t)c->p.loops));
+        SQ_HIP(hipMalloc(&c->g_cand, sq::qm1d_gs_cand_bytes(c->p.loops)));
+        SQ_HIP(hipMalloc(&c->g_flags, sizeof(int) * (size_t)c->p.loops));
+        SQ_HIP(hipMemset(c->g_flags, 0, sizeof(int) * (size_t)c->p.loops));
+        c->gs_tag = 0;
         c->g_loops = c->p.loops;
     }
     if (!c->g_st) SQ_HIP(hipMalloc(&c->g_st, sizeof(sq::Qm1dGsState)));
@@ -673,6 +684,10 @@ int qm1d_gs_frame(sq_ctx *c, int *stable) {
     a.xi = c->g_xi;
     a.om = c->g_om;
     a.xc = c->g_xc;
+    a.cand = c->g_cand;
+    a.flags = c->g_flags;
+    c->gs_tag = c->gs_tag == 0x7fffffff ? 1 : c->gs_tag + 1;
+    a.tag = c->gs_tag;
     a.hist = c->g_hist_buf;
     a.st = c->g_st;
     a.N = c->N;
@@ -913,6 +928,8 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->g_w2);
     (void)hipFree(c->g_seeds);
     (void)hipFree(c->g_lcg_scr);
+    (void)hipFree(c->g_cand);
+    (void)hipFree(c->g_flags);
     (void)hipFree(c->g_st);
     (void)hipFree(c->flag);
     (void)hipFree(c->dacc);

@@ -92,7 +92,9 @@ struct Qm1dGsState {
     int lrgEl, stable, steps_done;
     int rows_ready;      // steps the sweep has completed (sweep -> scan handshake; 0 at upload)
     long long consumed;  // random() calls the launch made (the shared seed advances by these)
-    int sync_error, pad; // the scan timed out waiting for the sweep
+    int sync_error;      // the scan timed out waiting for the sweep
+    int brk_step, brk_item;  // the serial break (-1: stable frame)
+    int pad;
 };
 
 struct Qm1dGsArgs {
@@ -103,6 +105,9 @@ struct Qm1dGsArgs {
     double *om;                    // omega at the start of each step (loops+1)
     double *xc;                    // potID 3: x_cl(i a, om[j]) at [j (N+2) + i + 1], i = -1..N,
                                    // then ddPot of it at the same index + (N+2) loops
+    void *cand;                    // per-step scan candidates (qm1d_gs_cand_bytes)
+    int *flags;                    // per-step "candidates ready" flags (== tag)
+    int tag;                       // this frame's flag value (never 0)
     double *hist;                  // field after each step (loops*N)
     Qm1dGsState *st;
     int N, pot, loops, runs;
@@ -119,6 +124,7 @@ constexpr size_t kLcgScratch = 3 * (size_t)kLcgChunks + 1;
 hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, uint32_t *w1,
                               uint32_t *w2, unsigned long long *seeds, double *xi,
                               unsigned long long *scr, hipStream_t s);
+size_t qm1d_gs_cand_bytes(int loops);
 hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s);
 
 // -------------------------------------------------------------- selftest --

@@ -922,6 +922,392 @@ __device__ __forceinline__ void gs_scan_mw(const Qm1dGsArgs &A, double *lds, int
     }
 }
 
+// ------------------------------------------------ scan by candidates ----
+// The scan's only step-to-step state is (E, V).  V_j is the running maximum
+// of |X| over the previous steps, independent of E; and E after a step is a
+// last leader, i.e. the first position of the maximum of X over a suffix of
+// that step's row: E_{j+1} is a suffix record of row j (X_i >= X_k for all
+// k > i).  Rows have few suffix records (about ln N for a random row, one for
+// the rising kink of potID 3), so every step is evaluated in parallel for
+// every candidate E (the previous row's suffix records, the state's E at step
+// 0), V-free: the candidate's next E and the leaders that are unstable for
+// some V -- the leaders with D > max_{k<i}|X_k| at which D is a running
+// maximum over those leaders; the first unstable leader for a given V is the
+// first of these with D > V.  One wave then walks the steps with a lookup per
+// step.  A row with more than kGsSlots candidates, or a candidate with more
+// than kGsRec such leaders, is evaluated directly by the walker with its
+// actual (E, V) -- the same routine, so the result is the same either way.
+constexpr int kGsSlots = 64;   // candidates per step (one per lane of the walker)
+constexpr int kGsRec = 4;      // unstable-leader records kept per candidate
+constexpr int kPrepBlocks = 32;
+
+struct GsCand {
+    int4 a;                // x: candidate E, y: E after the step, z: records (-1: overflow)
+    int4 ri;               // record sites
+    double2 rdp[kGsRec];   // record (D_i, max_{k<=i} |X_k|)
+};
+
+__device__ __forceinline__ GsCand *gs_cand(const Qm1dGsArgs &A, int j) {
+    return (GsCand *)A.cand + (size_t)j * kGsSlots;
+}
+__device__ __forceinline__ int *gs_nslot(const Qm1dGsArgs &A) {
+    return (int *)((GsCand *)A.cand + (size_t)A.loops * kGsSlots);
+}
+__device__ __forceinline__ double *gs_rowmax(const Qm1dGsArgs &A) {
+    return (double *)(gs_nslot(A) + ((A.loops + 1) & ~1));
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+struct GsEval {
+    int ll;       // last leader of the step (-1: none)
+    int nrec;     // unstable-leader records (-1: more than kGsRec)
+    int fb;       // first unstable item for the query V (kNone: none)
+    int ri[kGsRec];
+    double rd[kGsRec], rp[kGsRec];
+    double vbad;    // V after a break at fb
+    double rowmax;  // max |X| over the row
+};
+constexpr int kNone = 0x7fffffff;
+
+// Step j of the scan for a given E (one wave; same expressions and order as
+// gs_scan_reg per item): leaders, the first unstable item for V = Vq, and the
+// V-free records.
+__device__ GsEval gs_eval_step(const Qm1dGsArgs &A, int j, int E, double Vq) {
+    const int N = A.N, lane = threadIdx.x & 63;
+    const double NEG = -__builtin_inf();
+    const bool p3 = A.pot == 3;
+    const double *nrow = A.hist + (size_t)j * N;
+    const double *frow = j > 0 ? A.hist + (size_t)(j - 1) * N : A.f0;
+    const double *xr = A.xi + (size_t)j * (N + 1);
+    const double *cr = A.xc + (size_t)j * (N + 2) + 1;
+    const double nfE = j == 0 ? A.nfp[E] : frow[E];
+    const double T0 = nfE + (p3 ? cr[E] : 0.);
+    double m1 = NEG;
+    for (int c0 = 0; c0 < E; c0 += 64) {
+        const int i = c0 + lane;
+        if (i < E) m1 = fmax(m1, nrow[i] + (p3 ? cr[i] : 0.));
+    }
+    const bool caseB = dpp_all_max(m1) > T0;  // a leader before E: no reset at item E
+    const double base = caseB ? T0 : NEG;
+    GsEval r;
+    r.ll = -1;
+    r.nrec = 0;
+    r.fb = kNone;
+    r.vbad = 0.;
+#pragma unroll
+    for (int q = 0; q < kGsRec; ++q) {
+        r.ri[q] = 0;
+        r.rd[q] = r.rp[q] = 0.;
+    }
+    double cpy = NEG, cpa = NEG, cd = NEG;  // carries: max Y, max |X|, max D over the filtered leaders
+    for (int c0 = 0; c0 < N; c0 += 64) {
+        const int i = c0 + lane;
+        const bool in = i < N;
+        const double n = in ? nrow[i] : 0., f = in ? frow[i] : 0., xi = in ? xr[i] : 0.;
+        const double X = n + ((p3 && in) ? cr[i] : 0.);
+        const double AX = in ? absol(X) : NEG;
+        const double D = absol(n - f - A.sig * xi);  // :139, |nf - f - dw|
+        const double Y = (in && (caseB || i >= E)) ? X : NEG;
+        const double py = fmax(cpy, dpp_excl_max(Y));
+        const double pa = fmax(cpa, dpp_excl_max(AX));
+        const bool lead = in && (caseB || i > E) && X > fmax(base, py);
+        const double Vi = fmax(Vq, pa);
+        const uint64_t bq = __ballot(lead && D > Vi);
+        if (bq != 0ull && r.fb == kNone) {
+            const int l = __builtin_ctzll(bq);
+            r.fb = c0 + l;
+            r.vbad = readlane_d(fmax(Vi, AX), l);
+        }
+        const bool filt = lead && D > pa;
+        const double Dm = filt ? D : NEG;
+        const double dpre = fmax(cd, dpp_excl_max(Dm));
+        uint64_t br = __ballot(filt && D > dpre);
+        const double pinc = fmax(pa, AX);
+        while (br != 0ull) {
+            const int l = __builtin_ctzll(br);
+            br &= br - 1;
+            if (r.nrec < 0) break;
+            if (r.nrec == kGsRec) {
+                r.nrec = -1;
+                break;
+            }
+            const int ii = c0 + l;
+            const double dd = readlane_d(D, l), pp = readlane_d(pinc, l);
+#pragma unroll
+            for (int q = 0; q < kGsRec; ++q) {
+                if (q == r.nrec) {
+                    r.ri[q] = ii;
+                    r.rd[q] = dd;
+                    r.rp[q] = pp;
+                }
+            }
+            ++r.nrec;
+        }
+        const uint64_t bl = __ballot(lead);
+        if (bl != 0ull) r.ll = c0 + 63 - __builtin_clzll(bl);
+        cpy = fmax(cpy, dpp_all_max(Y));
+        cpa = fmax(cpa, dpp_all_max(AX));
+        cd = fmax(cd, dpp_all_max(Dm));
+    }
+    r.rowmax = cpa;
+    return r;
+}
+
+// The suffix records of row jr (X_i >= X_k for every k > i) into out[];
+// their number, or -1 when there are more than kGsSlots.  One wave.
+__device__ int gs_suffix_records(const Qm1dGsArgs &A, int jr, int *out) {
+    const int N = A.N, lane = threadIdx.x & 63;
+    const double NEG = -__builtin_inf();
+    const bool p3 = A.pot == 3;
+    const double *nrow = A.hist + (size_t)jr * N;
+    const double *cr = A.xc + (size_t)jr * (N + 2) + 1;
+    double carry = NEG;  // max X right of the current chunk
+    int cnt = 0;
+    for (int hi = N; hi > 0; hi -= 64) {
+        const int i = hi - 1 - lane;  // lanes walk the chunk right to left
+        const bool in = i >= 0;
+        const double X = in ? nrow[i] + (p3 ? cr[i] : 0.) : NEG;
+        const double right = fmax(carry, dpp_excl_max(X));  // max over k > i
+        const uint64_t rec = __ballot(in && X >= right);
+        const int c = __builtin_popcountll(rec);
+        if (cnt + c > kGsSlots) return -1;
+        if ((rec >> lane) & 1ull) out[cnt + __builtin_popcountll(rec & ((1ull << lane) - 1ull))] = i;
+        cnt += c;
+        carry = fmax(carry, dpp_all_max(X));
+    }
+    return cnt;
+}
+
+// Prep block k of K: rows j = k, k+K, ... as the sweep completes them.
+__device__ void gs_prep(const Qm1dGsArgs &A, int k, int K, int nthreads) {
+    __shared__ int s_cand[kGsSlots];
+    __shared__ int s_ns;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, W = nthreads >> 6;
+    int avail = 0;
+    for (int j = k; j < A.loops; j += K) {
+        if (!gs_wait_rows(A, j + 1, avail)) {
+            if (threadIdx.x == 0) A.st->sync_error = 1;
+            return;
+        }
+        if (wv == 0) {
+            int ns = 1;
+            if (j == 0) {
+                if (lane == 0) s_cand[0] = A.st->lrgEl;
+            } else {
+                ns = gs_suffix_records(A, j - 1, s_cand);
+            }
+            if (lane == 0) {
+                s_ns = ns;
+                gs_nslot(A)[j] = ns;
+            }
+        }
+        __syncthreads();
+        const int ns = s_ns;
+        for (int s = wv; s < ns; s += W) {
+            const int E = s_cand[s];
+            const GsEval r = gs_eval_step(A, j, E, __builtin_inf());
+            if (lane == 0) {
+                GsCand c;
+                c.a = make_int4(E, r.ll >= 0 ? r.ll : E, r.nrec, 0);
+                c.ri = make_int4(r.ri[0], r.ri[1], r.ri[2], r.ri[3]);
+#pragma unroll
+                for (int q = 0; q < kGsRec; ++q) c.rdp[q] = make_double2(r.rd[q], r.rp[q]);
+                gs_cand(A, j)[s] = c;
+                if (s == 0) gs_rowmax(A)[j] = r.rowmax;
+            }
+        }
+        // row j's candidates are complete: release them to the walker
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __syncthreads();  // (also: s_cand / s_ns are rewritten for the next row)
+        if (threadIdx.x == 0) __hip_atomic_store(&A.flags[j], A.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// One wave walks the steps as their candidates appear: per step the
+// candidate equal to E (a ballot over the lanes, which hold the step's
+// candidates), then its records against V.  Rows are taken in batches of
+// kWalkBatch: one flag wait, one acquire and one round of loads per batch.
+constexpr int kWalkBatch = 8;
+
+__device__ void gs_walk(const Qm1dGsArgs &A) {
+    __shared__ GsCand s_wc[kWalkBatch][kGsSlots];  // the batch's candidates, read at the matched slot
+    const int N = A.N, loops = A.loops, lane = threadIdx.x & 63;
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl;
+    int brk_step = -1, brk_item = -1;
+    bool done = false;
+    for (int j0 = 0; j0 < loops && !done; j0 += kWalkBatch) {
+        const int nb = min(kWalkBatch, loops - j0);
+        // wait for the batch's rows (lane q watches row j0 + q)
+        long long spins = 0;
+        while (true) {
+            const bool ok = lane >= nb ||
+                            __hip_atomic_load(&A.flags[j0 + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == A.tag;
+            if (__ballot(!ok) == 0ull) break;
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1ll << 25)) {
+                if (lane == 0) A.st->sync_error = 1;
+                return;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        int ns[kWalkBatch], ce[kWalkBatch];
+        double rm[kWalkBatch];
+#pragma unroll
+        for (int q = 0; q < kWalkBatch; ++q) {
+            const int j = min(j0 + q, loops - 1);
+            ns[q] = gs_nslot(A)[j];
+            rm[q] = gs_rowmax(A)[j];
+            const GsCand c = gs_cand(A, j)[lane];
+            ce[q] = c.a.x;
+            s_wc[q][lane] = c;
+        }
+        __builtin_amdgcn_wave_barrier();  // (one wave: LDS writes precede the reads below)
+#pragma unroll
+        for (int q = 0; q < kWalkBatch; ++q) {
+            const int j = j0 + q;
+            if (q >= nb || done) break;
+            const uint64_t m = ns[q] > 0 ? __ballot(lane < ns[q] && ce[q] == E) : 0ull;
+            int fb = kNone, en = E;
+            double vbad = 0., rmax = 0.;
+            bool direct = m == 0ull;
+            if (!direct) {
+                const GsCand &c = s_wc[q][__builtin_ctzll(m)];
+                en = c.a.y;
+                const int nrec = c.a.z;
+                rmax = rm[q];
+                if (nrec < 0) {
+                    direct = true;
+                } else {
+                    const int rr[kGsRec] = {c.ri.x, c.ri.y, c.ri.z, c.ri.w};
+#pragma unroll
+                    for (int q2 = 0; q2 < kGsRec; ++q2) {
+                        if (q2 < nrec && fb == kNone && c.rdp[q2].x > V) {
+                            fb = rr[q2];
+                            vbad = fmax(V, c.rdp[q2].y);
+                        }
+                    }
+                }
+            }
+            if (direct) {  // the step itself, with the actual E and V
+                const GsEval r = gs_eval_step(A, j, E, V);
+                fb = r.fb;
+                vbad = r.vbad;
+                en = r.ll >= 0 ? r.ll : E;
+                rmax = r.rowmax;
+            }
+            if (fb != kNone && j > 0) {  // items after fb see stable != 1 and never run this round
+                E = fb;
+                V = vbad;
+                brk_step = j;
+                brk_item = fb;
+                done = true;
+            } else {
+                E = en;
+                V = fmax(V, rmax);
+                if (fb != kNone) {  // round 0: the stable test only starts at round 1 (:168-171)
+                    brk_step = 0;
+                    brk_item = N;
+                    done = true;
+                }
+            }
+        }
+    }
+    // the persistent newf buffer (never rolled back, tauhost.c): the last
+    // step's field, or at a break the break step's field up to the breaking
+    // item and the previous step's after it
+    for (int i = lane; i < N; i += 64) {
+        if (brk_step < 0) A.nfp[i] = A.hist[(size_t)(loops - 1) * N + i];
+        else if (i <= brk_item) A.nfp[i] = A.hist[(size_t)brk_step * N + i];
+        else if (brk_step > 0) A.nfp[i] = A.hist[(size_t)(brk_step - 1) * N + i];
+    }
+    if (lane == 0) {
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = brk_step < 0 ? 1 : 0;
+        A.st->steps_done = brk_step < 0 ? loops : brk_step + 1;
+        A.st->omega_out = A.om[loops];
+        A.st->consumed = brk_step < 0 ? (long long)loops * (N + 1) : (long long)brk_step * (N + 1) + brk_item + 1;
+        A.st->brk_step = brk_step;
+        A.st->brk_item = brk_item;
+    }
+}
+
+// The running means of :144-145 for sites [i0, i0 + 256), over every step
+// as the sweep completes it (the same recurrences and operand order as the
+// scan kernels).  Written to the frame's new x / xx0 / f, which the host
+// adopts only if the frame is stable.
+constexpr int kMeansBatch = 8;
+__device__ void gs_means(const Qm1dGsArgs &A, int i0) {
+    const int N = A.N, loops = A.loops, mid = N / 2;
+    const int i = i0 + (int)threadIdx.x;
+    const bool in = i < N;
+    const int ic = in ? i : N - 1;
+    const bool p3 = A.pot == 3;
+    double x = A.x0[ic], xx = A.xx00[ic], f = A.f0[ic], fmo = A.f0[mid];
+    int avail = 0;
+    for (int j0 = 0; j0 < loops; j0 += kMeansBatch) {
+        const int nb = min(kMeansBatch, loops - j0);
+        if (!gs_wait_rows(A, j0 + nb, avail)) {
+            if (threadIdx.x == 0) A.st->sync_error = 1;
+            return;
+        }
+        double cn[kMeansBatch], cm[kMeansBatch], cc[kMeansBatch], ccm[kMeansBatch];
+#pragma unroll
+        for (int q = 0; q < kMeansBatch; ++q) {
+            const int j = min(j0 + q, loops - 1);
+            cn[q] = A.hist[(size_t)j * N + ic];
+            cm[q] = A.hist[(size_t)j * N + mid];
+            cc[q] = p3 ? A.xc[(size_t)j * (N + 2) + 1 + ic] : 0.;
+            ccm[q] = p3 ? A.xc[(size_t)j * (N + 2) + 1 + mid] : 0.;
+        }
+#pragma unroll
+        for (int q = 0; q < kMeansBatch; ++q) {
+            const int j = j0 + q;
+            if (q >= nb) break;
+            const double den = (double)(A.runs + j + 1);
+            const double g = f + cc[q];
+            const double fm = (i > mid && j < loops - 1) ? cm[q] : fmo;
+            xx = xx + (g * (fm + ccm[q]) - xx) / den;
+            x = x + (g - x) / den;
+            f = cn[q];
+            fmo = cm[q];
+        }
+    }
+    if (in) {
+        A.nf[i] = f;
+        A.nx[i] = x;
+        A.nxx0[i] = xx;
+    }
+}
+
+// One frame: the sweep (block 0, XCD 0), candidate prep, running means and
+// the walk, all concurrently.  Blocks b with b % 8 == 0 (XCD 0, round-robin
+// dispatch) other than 0 stay idle so that the other roles' acquires do not
+// invalidate the sweep's L2.
+__host__ __device__ constexpr int gs_role_blocks(int need) {  // grid size giving `need` non-XCD-0 blocks
+    return 1 + need + (need + 6) / 7;
+}
+
+template <int CH, bool P3>
+__global__ __launch_bounds__(1024) void gs_frame_cand_kernel(const Qm1dGsArgs A, int B, int sweep_threads,
+                                                             int publish, int nprep, int nmeans) {
+    const int b = (int)blockIdx.x;
+    if (b == 0) {
+        if ((int)threadIdx.x < sweep_threads) gs_sweep<CH, P3>(A, B, sweep_threads, publish);
+        return;
+    }
+    if ((b & 7) == 0 || threadIdx.x >= 256) return;
+    const int k = b - 1 - (b >> 3);  // index among the non-XCD-0 blocks
+    if (k < nprep) gs_prep(A, k, nprep, 256);
+    else if (k < nprep + nmeans) gs_means(A, (k - nprep) * 256);
+    else if (k == nprep + nmeans && threadIdx.x < 64) gs_walk(A);
+}
+
 // One frame's sweep (block 0) and scan (block 1), concurrently.  Waves past
 // a block's own thread count exit at once.  SC: scan variant (0: one wave,
 // 2 sites per lane; 1: one wave, 4; 2: multi-wave).
@@ -964,6 +1350,11 @@ hipError_t qm1d_gs_lcg_launch(unsigned long long seed, int N, long long ncalls, 
     return hipGetLastError();
 }
 
+size_t qm1d_gs_cand_bytes(int loops) {
+    return sizeof(GsCand) * kGsSlots * (size_t)loops + sizeof(int) * (size_t)((loops + 1) & ~1) +
+           sizeof(double) * (size_t)loops;  // + the per-row flags, allocated apart
+}
+
 hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     const int B = qm1d_gs_block(a.N);
     if (B == 0) return hipErrorInvalidValue;
@@ -995,14 +1386,30 @@ hipError_t qm1d_gs_frame_launch(const Qm1dGsArgs &a, hipStream_t s) {
     // scan: one wave up to 256 sites (measured faster than two waves with barriers),
     // else 2 sites per thread up to 2048 sites (16 waves), up to 4 beyond
     const int scan_threads = a.N <= 256 ? 64 : 64 * std::min(16, (a.N + 127) / 128);
-    const dim3 grid(2), block(std::max(sweep_threads, scan_threads));
-    const size_t lds2 = 2 * lds1;
-    const bool p3 = a.pot == 3;
     static const int publish = [] {
         const char *e = getenv("SQ_GS_PUBLISH");
         const int v = e ? atoi(e) : 0;
         return v > 0 ? v : kPublishEvery;
     }();
+    static const bool seq_scan = [] {
+        const char *e = getenv("SQ_GS_SCAN");
+        return e != nullptr && e[0] == 's';
+    }();
+    if (!seq_scan) {  // sweep + candidate prep, then the walk and the outputs
+        const int nprep = kPrepBlocks, nmeans = (a.N + 255) / 256;
+        const dim3 g2(gs_role_blocks(nprep + nmeans + 1)), b2(std::max(sweep_threads, 256));
+#define SQ_GS_CAND(CH, P3) \
+    hipLaunchKernelGGL((gs_frame_cand_kernel<CH, P3>), g2, b2, 0, s, a, B, sweep_threads, publish, nprep, nmeans)
+        if (B <= 2 && a.pot == 3) SQ_GS_CAND(2, true);
+        else if (B <= 2) SQ_GS_CAND(2, false);
+        else if (a.pot == 3) SQ_GS_CAND(4, true);
+        else SQ_GS_CAND(4, false);
+#undef SQ_GS_CAND
+        return hipGetLastError();
+    }
+    const dim3 grid(2), block(std::max(sweep_threads, scan_threads));
+    const size_t lds2 = 2 * lds1;
+    const bool p3 = a.pot == 3;
 #define SQ_GS_FRAME(CH, SC)                                                                                     \
     hipLaunchKernelGGL((p3 ? gs_frame_kernel<CH, true, SC> : gs_frame_kernel<CH, false, SC>), grid, block, lds2, \
                        s, a, B, sweep_threads, scan_threads, publish)
