@@ -479,12 +479,14 @@ int create_phi4(sq_ctx *c) {
     }
     if (const char *e = getenv("SQ_VSEG"))  // tuning override: float4 segments per lane
         if (atoi(e) == 1 || (atoi(e) == 2 && c->geom.qx == 64 && c->Lx % 512 == 0)) c->geom.v = atoi(e);
-    {   // both fields (in + out) beyond ~3/4 of the 256 MiB Infinity Cache: stream the output
+    {   // very large per-device fields: non-temporal output stores (mode 4) beat the
+        // sc0 sc1 stores of mode 7 at 1024^3 (1575 vs 1598 us per step), not at
+        // 512^3 (193.5 vs 190.8 us), profiles/r01/sweep*_sc1.log
         const long long nz_dev = p.comm == SQ_COMM_RCCL ? (c->Lz + p.nranks - 1) / std::max(1, p.nranks) : c->Lz;
         const double field_bytes = 4.0 * c->Lx * c->Ly * (double)nz_dev;  // this device's share
-        if (c->geom.pf == 3 && 2.0 * field_bytes > 192.0 * (1 << 20)) c->geom.pf = 4;
+        if (c->geom.pf == 7 && 2.0 * field_bytes > 2.0 * (1 << 30)) c->geom.pf = 4;
     }
-    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = (atoi(e) >= 1 && atoi(e) <= 5) ? atoi(e) : 1;
+    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = (atoi(e) >= 1 && atoi(e) <= 7) ? atoi(e) : 1;
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;

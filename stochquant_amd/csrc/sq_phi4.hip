@@ -386,7 +386,10 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
         // keeping it out of L2/MALL leaves them to the input's halo reuse):
         // 512^3 199.7 -> 186.8 us, 1024^3 1606 -> 1570 us; at 256^3 (MALL-
         // resident) it costs 21.6 -> 30.0 us (profiles/r01/sweep*_ntstore.log)
-        constexpr int SAUX = PF == 4 ? 2 : 0;
+        // PF == 6 / 7: sc1 / sc0 sc1 output stores (write-through that drops
+        // the line from the XCD's L2, guide table "stores of each flavour"), so
+        // the output does not evict the input rows other waves re-read
+        constexpr int SAUX = PF == 4 ? 2 : PF == 6 ? 16 : PF == 7 ? 17 : 0;
         for (int z = zbeg; z < zend; z += 3) {
             plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
             if (z + 1 >= zend) break;
@@ -507,8 +510,12 @@ bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     const int v = (qx == 64 && Lx % 512 == 0) ? 2 : 1;
     // full-row waves use packed-f32 site arithmetic (queue mode 3): bit-identical,
     // 15 % fewer VALU instructions, measured 256^3 22.3 -> 21.3 us, 512^3
-    // 196.5 -> 193.4 us (profiles/r01/sweep*_packed.log)
-    const int pf = qx == 64 ? 3 : 1;
+    // 196.5 -> 193.4 us (profiles/r01/sweep*_packed.log); and (mode 7) write
+    // their output with sc0 sc1 stores, which leave the XCD's L2 at once
+    // instead of occupying the lines other waves' halo rows are re-read from:
+    // 256^3 21.66 -> 20.98 us per step, 512^3 193.1 -> 190.8 us (faster than
+    // the non-temporal stores of mode 4 there), profiles/r01/sweep*_sc1.log
+    const int pf = qx == 64 ? 7 : 1;
     const bool narrow = Lx <= 256;
     const int rcand[3] = {narrow ? 1 : 2, narrow ? 2 : 4, narrow ? 4 : 1};
     for (int r : rcand) {  // a full wave tile that divides Ly
@@ -557,6 +564,12 @@ static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hi
         if (pf == 4)
             return nz ? launch_pf<QX, R, V, MS, true, 4>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 4>(a, grid, s, e0, e1);
+        if (pf == 6)
+            return nz ? launch_pf<QX, R, V, MS, true, 6>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 6>(a, grid, s, e0, e1);
+        if (pf == 7)
+            return nz ? launch_pf<QX, R, V, MS, true, 7>(a, grid, s, e0, e1)
+                      : launch_pf<QX, R, V, MS, false, 7>(a, grid, s, e0, e1);
         // LH needs each block's 4 waves to be 4 y-adjacent groups of one z-chunk
         if constexpr (!MS) {
             if (pf == 5 && a.nxseg == 1 && a.nyg % 4 == 0)

@@ -241,7 +241,7 @@ def test_rccl_self_exchange_deep_halo_frames(gpu, oracle_mod, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(256, 8, 8), (256, 4, 33), (512, 4, 6), (256, 16, 5)])
-@pytest.mark.parametrize("pf", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("pf", [1, 2, 3, 4, 5, 6, 7])
 def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     monkeypatch.setenv("SQ_PREFETCH", str(pf))
     phi0 = _init(oracle_mod, shape)
