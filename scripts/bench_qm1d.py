@@ -23,13 +23,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=5)
     ap.add_argument("--ordering", default="serial", choices=["serial", "jacobi"])
+    ap.add_argument("--no-cpu", action="store_true", help="GPU timings only (no oracle run)")
+    ap.add_argument("--no-c1", action="store_true", help="skip config C1's 32,768-site chain")
     a = ap.parse_args()
     import oracle
     from stochquant_amd import Qm1dChain
     # (N, dt, dtau, potID, loops): taumain.py presets' shapes and the C1-like chain
     shapes = [(100, 0.1, 0.002, 3, 1000), (200, 0.1, 0.002, 3, 200), (1000, 0.05, 0.0005, 0, 1000),
               (3072, 0.05, 0.0005, 0, 200)]
-    if a.ordering == "jacobi":
+    if a.ordering == "jacobi" and not a.no_cpu and not a.no_c1:
         shapes.append((32768, 1.0, 0.01, 0, 1000))  # config C1
     for N, dt, dtau, pot, loops in shapes:
         f0 = 0.1 * np.random.default_rng(1).standard_normal(N)
@@ -42,6 +44,10 @@ def main():
             st = [g.run_frame() for _ in range(a.frames)]
             g.sync()
             gpu_ms = (time.perf_counter() - t0) * 1e3 / a.frames
+        if a.no_cpu:
+            print(json.dumps({"ordering": a.ordering, "N": N, "loops": loops, "pot": pot, "stable_frames": int(sum(st)),
+                              "gpu_ms_per_frame": round(gpu_ms, 3), "qm1d_k": os.environ.get("SQ_QM1D_K")}), flush=True)
+            continue
         nf = max(1, min(a.frames, int(2e6 // (N * loops)) or 1))
         if a.ordering == "serial":
             ch = oracle.SerialChain(N, dt, dtau, pot, 1.0, loops, 12345, f0, omega=dt * (N // 2))

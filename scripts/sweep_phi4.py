@@ -24,16 +24,20 @@ def main():
     ap.add_argument("--zc", default="2,4,8,16")
     ap.add_argument("--pf", default="1", help="z prefetch distances to try (1,2)")
     ap.add_argument("--vseg", default="0", help="float4 segments per lane to try (0 = library default)")
+    ap.add_argument("--wpb", default="4", help="waves per block to try (needs a build with SQ_WPB; "
+                                               "measured no gain, profiles/r01/sweep*_wpb.log)")
     ap.add_argument("--C", type=float, default=1.0, help="noise amplitude (0: RNG-free gradient-flow kernel)")
     a = ap.parse_args()
     from stochquant_amd import Phi4Lattice
     L = a.size
     variants = list(itertools.product([int(r) for r in a.rows.split(",")], [int(z) for z in a.zc.split(",")],
-                                      [int(p) for p in a.pf.split(",")], [int(v) for v in a.vseg.split(",")]))
+                                      [int(p) for p in a.pf.split(",")], [int(v) for v in a.vseg.split(",")],
+                                      [int(w) for w in a.wpb.split(",")]))
     res = {v: [] for v in variants}
     lats = {}
     for v in variants:
         os.environ["SQ_ROWS"], os.environ["SQ_ZCHUNK"], os.environ["SQ_PREFETCH"] = str(v[0]), str(v[1]), str(v[2])
+        os.environ["SQ_WPB"] = str(v[4])
         if v[3]:
             os.environ["SQ_VSEG"] = str(v[3])
         else:
@@ -46,7 +50,7 @@ def main():
     for rnd in range(a.rounds):
         for v in variants:
             lat = lats[v]
-            row = {"rows": v[0], "zc": v[1], "pf": v[2], "vseg": v[3], "round": rnd}
+            row = {"rows": v[0], "zc": v[1], "pf": v[2], "vseg": v[3], "wpb": v[4], "round": rnd}
             for mode in (0, 1, 2):
                 lat.perf_reset()
                 lat.set_profiling(mode)
@@ -66,7 +70,7 @@ def main():
     for v in sorted(variants, key=lambda v: statistics.median(k for k, _ in res[v])):
         k = statistics.median(x for x, _ in res[v])
         w = statistics.median(y for _, y in res[v])
-        print(f"rows={v[0]} zc={v[1]:3d} pf={v[2]} v={v[3]}  kernel {k:8.3f} us  wall {w:8.3f} us  {8 * L ** 3 / (k * 1e-6) / 1e9:8.1f} GB/s")
+        print(f"rows={v[0]} zc={v[1]:3d} pf={v[2]} v={v[3]} wpb={v[4]}  kernel {k:8.3f} us  wall {w:8.3f} us  {8 * L ** 3 / (k * 1e-6) / 1e9:8.1f} GB/s")
     for lat in lats.values():
         lat.close()
 

@@ -95,7 +95,7 @@ struct sq_ctx {
     double *qf[2] = {nullptr, nullptr}, *qx[2] = {nullptr, nullptr}, *qxx0[2] = {nullptr, nullptr};
     int qcur = 0;
     sq::Qm1dState *qst = nullptr;
-    double *qscr[3] = {nullptr, nullptr, nullptr};  // N > 8192: fs, xs, ds of Qm1dArgs
+    double *qscr[3] = {nullptr, nullptr, nullptr};  // N > kQm1dRegMaxN: fs, xs, ds of Qm1dArgs
     double omega = 0;
     long runs = 0;
     int lrgEl = 0;
@@ -602,7 +602,7 @@ int create_qm1d(sq_ctx *c) {
         SQ_HIP(hipMemset(c->qx[k], 0, bytes));
         SQ_HIP(hipMemset(c->qxx0[k], 0, bytes));
     }
-    if (sq::qm1d_sites_per_thread(c->N) > 8)  // global-memory variant: f ping-pong + scan scratch
+    if (c->N > sq::kQm1dRegMaxN)  // global-memory variant: f ping-pong + scan scratch
         for (double **q : {&c->qscr[0], &c->qscr[1], &c->qscr[2]}) SQ_HIP(hipMalloc(q, bytes));
     SQ_HIP(hipMalloc(&c->qst, sizeof(sq::Qm1dState)));
     SQ_HIP(hipStreamCreateWithFlags(&c->qstream, hipStreamNonBlocking));

@@ -1,0 +1,64 @@
+// sq_dpp.h -- wave-level helpers on DPP lane moves (no LDS round trips),
+// shared by the QM1D kernels (sq_qm1d.hip, sq_qm1d_gs.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace sq {
+namespace {
+
+// Wave-wide max-scans by DPP (row_shr 1/2/4/8, row_bcast 15/31: the gfx9
+// inclusive-scan sequence), no LDS round trips; 64-bit values move as two
+// 32-bit DPP halves.  Out-of-range lanes read the identity (bound_ctrl off).
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_d(double v, double id) {
+    const int lo = __builtin_amdgcn_update_dpp((int)__double2loint(id), (int)__double2loint(v), CTRL, RM, BM, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)__double2hiint(id), (int)__double2hiint(v), CTRL, RM, BM, false);
+    return __hiloint2double(hi, lo);
+}
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ int dpp_i(int v, int id) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, RM, BM, false);
+}
+__device__ __forceinline__ double dpp_incl_max(double v) {
+    const double id = -__builtin_inf();
+    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x114, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x118, 0xf, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v, id));
+    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v, id));
+    return v;
+}
+__device__ __forceinline__ double dpp_excl_max(double v) {  // max over lanes < this lane
+    return dpp_d<0x138, 0xf, 0xf>(dpp_incl_max(v), -__builtin_inf());  // wave_shr:1
+}
+__device__ __forceinline__ double dpp_all_max(double v) {
+    const double s = dpp_incl_max(v);
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(s), 63),
+                            __builtin_amdgcn_readlane(__double2loint(s), 63));
+}
+__device__ __forceinline__ int dpp_all_max_i(int v) {
+    const int id = (int)0x80000000;
+    v = max(v, dpp_i<0x111, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x112, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x114, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x118, 0xf, 0xf>(v, id));
+    v = max(v, dpp_i<0x142, 0xa, 0xf>(v, id));
+    v = max(v, dpp_i<0x143, 0xc, 0xf>(v, id));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
+
+// lane l <- lane l-1 (wave_shr:1) / lane l+1 (wave_shl:1); the lane shifted
+// in from outside the wave keeps `id`
+__device__ __forceinline__ double dpp_from_left(double v, double id) { return dpp_d<0x138, 0xf, 0xf>(v, id); }
+__device__ __forceinline__ double dpp_from_right(double v, double id) { return dpp_d<0x130, 0xf, 0xf>(v, id); }
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                            __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+
+}  // namespace
+}  // namespace sq

@@ -37,7 +37,9 @@ struct Phi4Geom {
     int wy;   // rows per wave unit
     int pf;   // register queue: 1 prefetch distance 1; 2 distance 2 (qx == 64, v == 1);
               // 3 distance 1 + packed-f32 site arithmetic (qx == 64, the default there);
-              // 4 as 3 with non-temporal output stores (default when the fields exceed the MALL)
+              // 4 as 3 with non-temporal output stores (default above 2 GiB of fields per device);
+              // 5 as 3 with LDS-staged y-halo rows; 6 / 7 as 3 with sc1 / sc0 sc1 output
+              // stores (7: the default for full-row waves)
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 
@@ -74,7 +76,7 @@ struct Qm1dState {    // device-resident frame scalars
 struct Qm1dArgs {
     const double *f, *x, *xx0;  // frame-start state (N)
     double *nf, *nx, *nxx0;     // state after the frame (N)
-    double *fs, *xs, *ds;       // N > 8192 only: f ping-pong, X' and drift-check scratch (N each)
+    double *fs, *xs, *ds;       // N > kQm1dRegMaxN only: f ping-pong, X' and drift-check scratch (N each)
     Qm1dState *st;
     int N, pot, loops, runs;
     double a, a2, h, sig, sigw, kconst;
@@ -82,8 +84,9 @@ struct Qm1dArgs {
     unsigned long long tick;    // Philox step index of the frame's first step
 };
 
-int qm1d_sites_per_thread(int N);  // 0 if N unsupported; > 8 = global-memory variant
+int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant: N > kQm1dRegMaxN)
 constexpr int kQm1dMaxN = 1024 * 64;
+constexpr int kQm1dRegMaxN = 4096;  // register-resident frame kernel up to here; beyond, f ping-pong + scan scratch
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
 
 // QM1D in the reference's serial order (sq_qm1d_gs.hip)

@@ -17,6 +17,10 @@
 // scan partials go through LDS.  Expressions keep the reference's order and
 // the file is built with -ffp-contract=off, so for potID 0 the deterministic
 // part is bit-identical to the oracle.
+#include <algorithm>
+#include <cstdlib>
+
+#include "sq_dpp.h"
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -52,16 +56,43 @@ __device__ __forceinline__ double wave_incl_max(double v, int lane) {
 }
 
 template <int K>
-__global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs A) {
-    __shared__ double s_first[kMaxThreads], s_last[kMaxThreads];
-    __shared__ double s_wmaxX[kMaxThreads / 64], s_wmaxA[kMaxThreads / 64];
-    __shared__ double s_fmid, s_R;
-    __shared__ int s_leader[2];
+__device__ __forceinline__ double pick(const double (&v)[K], int k) {  // v[k], k wave-uniform
+    double r = v[0];
+#pragma unroll
+    for (int q = 1; q < K; ++q)
+        if (q == k) r = v[q];
+    return r;
+}
+
+// One frame, N <= 4,096: thread g (= 64 wave + lane) owns sites [gK, gK+K)
+// in registers; W = blockDim/64 <= 16 waves (MW) or one wave.  Per step:
+//   1. site updates from the old field (left/right neighbours by DPP wave
+//      shifts; across waves through LDS), running means, guard, X', drift
+//      check;
+//   2. the scan's maxima: lane max of X' (first index) and |X'|, DPP
+//      prefix maxima inside the wave, one LDS slot per wave across waves;
+//      the step's last leader is the first index of the maximum X' when that
+//      exceeds X'(E) (leaders are strict running-maximum records), V' =
+//      max(V, max |X'|), a site is an unstable leader iff X' exceeds every X'
+//      before it and X'(E) while its drift check exceeds V and every |X'|
+//      before it (oracle/orc_qm1d.c orc_qm1d_frame, tau_kernel.cl:135-143);
+//   3. omega from its counter-based normal (drawn 64 steps at a time, one
+//      step per lane, and read back with readlane).
+// One wave needs no barrier at all (readlane / ballot); W waves use two per
+// step, with the LDS slots double-buffered by step parity.
+template <int K, bool MW>
+__global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs A) {
+    constexpr int kW = 16;
+    __shared__ double s_first[2][kW], s_last[2][kW], s_mx[2][kW], s_ma[2][kW];
+    __shared__ int s_arg[2][kW], s_un[2][kW];
+    __shared__ double s_fmid[2], s_xe[2];
 
     const int N = A.N, pot = A.pot, mid = N / 2;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = blockDim.x >> 6;
-    const int i0 = t * K;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int W = MW ? (int)(blockDim.x >> 6) : 1;
+    const int i0 = (int)threadIdx.x * K;
     const double h = A.h, a = A.a, a2 = A.a2;
+    const double ninf = -__builtin_inf();
 
     double f[K], x[K], xx0[K], Xn[K], dchk[K];
 #pragma unroll
@@ -76,134 +107,168 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs 
     double V = A.st->lrgVl;
     int stable = 1, steps = 0;
 
+    // neighbours and f[mid] of the frame-start field
+    double fL = dpp_from_left(f[K - 1], 0.), fR = dpp_from_right(f[0], 0.), fmid;
+    if constexpr (MW) {
+        if (lane == 0) s_first[1][wv] = f[0];
+        if (lane == 63) s_last[1][wv] = f[K - 1];
+        if (mid / K == (int)threadIdx.x) s_fmid[1] = pick(f, mid % K);
+        __syncthreads();
+        if (lane == 0 && wv > 0) fL = s_last[1][wv - 1];
+        if (lane == 63 && wv + 1 < W) fR = s_first[1][wv + 1];
+        fmid = s_fmid[1];
+    } else {
+        fmid = readlane_d(pick(f, mid % K), mid / K);
+    }
+    float wnoise = 0.f;  // omega's normals for 64 steps, one step per lane
+
     for (int j = 0; j < A.loops; ++j) {
+        const int p = j & 1;
         const unsigned long long step = A.tick + (unsigned long long)j;
         const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-        // ---- phase 1: publish edges and f[mid] (old field) ----
-        s_first[t] = f[0];
-        s_last[t] = f[K - 1];
-#pragma unroll
-        for (int k = 0; k < K; ++k)
-            if (i0 + k == mid) s_fmid = f[k];
-        if (t == 0) s_leader[j & 1] = -1;
-        __syncthreads();
-        const double fL = t > 0 ? s_last[t - 1] : 0.;
-        const double fR = (t + 1 < (int)blockDim.x) ? s_first[t + 1] : 0.;
-        const double fmid = s_fmid;
-        const double Xm = fmid + xcl((double)mid * a, om, pot);
-        const double den = (double)(A.runs + j + 1);
-
-        // ---- phase 2: site updates ----
+        if ((j & 63) == 0) {
+            const unsigned long long sl = step + (unsigned long long)lane;
+            wnoise = normals4(0ull, kStreamOmega, (uint32_t)sl, (uint32_t)(sl >> 32), A.k0, A.k1).a;
+        }
+        // ---- 1. site updates ----
         float nz[K < 4 ? 4 : K];
         if constexpr (K >= 4) {
 #pragma unroll
             for (int q = 0; q < K / 4; ++q) {
-                const f32x4n n = normals4((unsigned long long)((i0 >> 2) + q), kStreamField, slo, shi,
-                                          A.k0, A.k1);
+                const f32x4n n = normals4((unsigned long long)((i0 >> 2) + q), kStreamField, slo, shi, A.k0, A.k1);
                 nz[4 * q] = n.a;
                 nz[4 * q + 1] = n.b;
                 nz[4 * q + 2] = n.c;
                 nz[4 * q + 3] = n.d;
             }
         } else {
+            const f32x4n n = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
+            const float q4[4] = {n.a, n.b, n.c, n.d};
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int i = i0 + k;
-                const f32x4n n = normals4((unsigned long long)(i >> 2), kStreamField, slo, shi, A.k0,
-                                          A.k1);
-                const int c = i & 3;
-                nz[k] = c == 0 ? n.a : c == 1 ? n.b : c == 2 ? n.c : n.d;
-            }
+            for (int k = 0; k < K; ++k) nz[k] = q4[(i0 & 3) + k];
         }
+        const double Xm = fmid + xcl((double)mid * a, om, pot);
+        const double den = (double)(A.runs + j + 1);
         double prev_old = fL;  // old f[i-1]
-        double lmaxX = -INFINITY, lmaxA = -INFINITY;
+        double lmaxX = ninf, lmaxA = ninf;
+        int larg = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             const int i = i0 + k;
-            if (i >= N) break;
-            const double fi = f[k];
-            const double xc = xcl((double)i * a, om, pot);
-            const double dw = A.sig * (double)nz[k];
-            const double fr = (k + 1 < K) ? f[k + 1] : fR;
-            double v;
-            if (i == 0)
-                v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
-                    ddpot(xc, pot) * fi * h + dw;
-            else if (i == N - 1)
-                v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
-                    ddpot(xc, pot) * fi * h + dw;
-            else
-                v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
-            if (v > 1000) v = 1000;  // guard, :119-133
-            if (v < -1000) v = -1000;
-            if (v != v) v = 1000;
-            dchk[k] = absol(v - fi - dw);
-            const double X = v + xc;
-            Xn[k] = X;
-            lmaxX = fmax(lmaxX, X);
-            lmaxA = fmax(lmaxA, absol(X));
-            // running means from the OLD field, :144-145
-            const double Xi = fi + xc;
-            xx0[k] = xx0[k] + (Xi * Xm - xx0[k]) / den;
-            x[k] = x[k] + (Xi - x[k]) / den;
-            prev_old = fi;
-            f[k] = v;
-        }
-        if (E >= i0 && E < i0 + K) {
-#pragma unroll
-            for (int k = 0; k < K; ++k)
-                if (i0 + k == E) s_R = Xn[k];
-        }
-        // ---- phase 3: block exclusive prefix max of X' and |X'| ----
-        const double ix = wave_incl_max(lmaxX, lane);
-        const double ia = wave_incl_max(lmaxA, lane);
-        double ex = __shfl_up(ix, 1, 64), ea = __shfl_up(ia, 1, 64);
-        if (lane == 0) {
-            ex = -INFINITY;
-            ea = -INFINITY;
-        }
-        if (lane == 63) {
-            s_wmaxX[wv] = ix;
-            s_wmaxA[wv] = ia;
-        }
-        __syncthreads();
-        double runX = s_R, runA = V, totA = V;
-        for (int w = 0; w < nw; ++w) {
-            const double wx = s_wmaxX[w], wa = s_wmaxA[w];
-            if (w < wv) {
-                runX = fmax(runX, wx);
-                runA = fmax(runA, wa);
+            Xn[k] = ninf;
+            dchk[k] = 0.;
+            if (i < N) {
+                const double fi = f[k];
+                const double xc = xcl((double)i * a, om, pot);
+                const double dw = A.sig * (double)nz[k];
+                const double fr = (k + 1 < K) ? f[k + 1] : fR;
+                double v;
+                if (i == 0)
+                    v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
+                        ddpot(xc, pot) * fi * h + dw;
+                else if (i == N - 1)
+                    v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
+                        ddpot(xc, pot) * fi * h + dw;
+                else
+                    v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
+                if (v > 1000) v = 1000;  // guard, :119-133
+                if (v < -1000) v = -1000;
+                if (v != v) v = 1000;
+                dchk[k] = absol(v - fi - dw);
+                const double X = v + xc;
+                Xn[k] = X;
+                if (X > lmaxX) {
+                    lmaxX = X;
+                    larg = i;
+                }
+                lmaxA = fmax(lmaxA, absol(X));
+                // running means from the OLD field, :144-145
+                const double Xi = fi + xc;
+                xx0[k] = xx0[k] + (Xi * Xm - xx0[k]) / den;
+                x[k] = x[k] + (Xi - x[k]) / den;
+                prev_old = fi;
+                f[k] = v;
             }
-            totA = fmax(totA, wa);
         }
-        runX = fmax(runX, ex);
-        runA = fmax(runA, ea);
-        int unst = 0, leader = -1;
+        // ---- 2. scan maxima ----
+        const double wmx = dpp_all_max(lmaxX), wma = dpp_all_max(lmaxA);
+        const unsigned long long hit = __ballot(lmaxX == wmx);
+        const int warg = __builtin_amdgcn_readlane(larg, (int)__builtin_ctzll(hit));
+        double XE, pX, pA, gX, totA;
+        int garg;
+        if constexpr (MW) {
+            if (lane == 0) {
+                s_mx[p][wv] = wmx;
+                s_ma[p][wv] = wma;
+                s_arg[p][wv] = warg;
+                s_first[p][wv] = f[0];
+            }
+            if (lane == 63) s_last[p][wv] = f[K - 1];
+            if (E / K == (int)threadIdx.x) s_xe[p] = pick(Xn, E % K);
+            if (mid / K == (int)threadIdx.x) s_fmid[p] = pick(f, mid % K);
+            __syncthreads();
+            XE = s_xe[p];
+            pX = XE;
+            pA = V;
+            gX = ninf;
+            garg = 0;
+            totA = V;
+            for (int w = 0; w < W; ++w) {
+                const double mx = s_mx[p][w], ma = s_ma[p][w];
+                if (w < wv) {
+                    pX = fmax(pX, mx);
+                    pA = fmax(pA, ma);
+                }
+                totA = fmax(totA, ma);
+                if (mx > gX) {
+                    gX = mx;
+                    garg = s_arg[p][w];
+                }
+            }
+        } else {
+            XE = readlane_d(pick(Xn, E % K), E / K);
+            pX = XE;
+            pA = V;
+            gX = wmx;
+            garg = warg;
+            totA = fmax(V, wma);
+        }
+        double runX = fmax(pX, dpp_excl_max(lmaxX)), runA = fmax(pA, dpp_excl_max(lmaxA));
+        int unst = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
-            const int i = i0 + k;
-            if (i >= N) break;
             if (Xn[k] > runX) {
                 runX = Xn[k];
-                leader = i;
                 if (dchk[k] > runA) unst = 1;
             }
             runA = fmax(runA, absol(Xn[k]));
         }
-        if (leader >= 0) atomicMax(&s_leader[j & 1], leader);
-        const int any_unst = __syncthreads_or(unst);
-        const int L = s_leader[j & 1];
-        if (L >= 0) E = L;
+        int any = __ballot(unst) != 0ull;
+        // neighbours of the new field for the next step
+        fL = dpp_from_left(f[K - 1], 0.);
+        fR = dpp_from_right(f[0], 0.);
+        if constexpr (MW) {
+            if (lane == 0) s_un[p][wv] = any;
+            if (lane == 0 && wv > 0) fL = s_last[p][wv - 1];
+            if (lane == 63 && wv + 1 < W) fR = s_first[p][wv + 1];
+            fmid = s_fmid[p];
+            __syncthreads();
+            any = 0;
+            for (int w = 0; w < W; ++w) any |= s_un[p][w];
+        } else {
+            fmid = readlane_d(pick(f, mid % K), mid / K);
+        }
+        if (gX > XE) E = garg;
         V = totA;
-        // ---- collective coordinate, :103-110,155-167 (uniform) ----
-        const f32x4n nwn = normals4(0ull, kStreamOmega, slo, shi, A.k0, A.k1);
-        const double nwo = om + A.kconst * (A.sigw * (double)nwn.a);
+        // ---- 3. collective coordinate, :103-110,155-167 (uniform) ----
+        const float xw = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wnoise), j & 63));
+        const double nwo = om + A.kconst * (A.sigw * (double)xw);
         const double top = (double)(N - 1) * a;
         if (nwo > top) om = 2 * (double)(N - 1) * a - nwo;
         else if (nwo < 0) om = -nwo;
         else om = nwo;
         steps = j + 1;
-        if (any_unst) {
+        if (any) {
             stable = 0;
             break;
         }
@@ -217,7 +282,7 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs 
             A.nxx0[i] = xx0[k];
         }
     }
-    if (t == 0) {
+    if (threadIdx.x == 0) {
         A.st->omega_out = om;
         A.st->lrgEl = E;
         A.st->lrgVl = V;
@@ -226,7 +291,7 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel(const Qm1dArgs 
     }
 }
 
-// The same frame for N > 8192 (config C1's 32,768-site chain): one work-group,
+// The same frame for N > 4096 (config C1's 32,768-site chain): one work-group,
 // K sites per thread held in global memory (L2-resident at these sizes)
 // instead of registers.  Every thread reads and writes only its own sites;
 // neighbour edges and f[mid] still go through LDS, so no cross-thread global
@@ -376,16 +441,53 @@ int qm1d_sites_per_thread(int N) {
     return 0;
 }
 
+// Register kernel shape for N <= 4,096: one wave with K <= 2 sites per lane
+// up to N = 128, one site per lane up to 256, then W = ceil(N/256) <= 16
+// waves with K = 4 (16 waves are 4 per SIMD, <= 128 VGPRs each: K = 8 would
+// spill).
+static bool qm1d_wave_shape(int N, int &K, int &W) {
+    if (N < 2 || N > kQm1dRegMaxN) return false;
+    static const int kforce = [] {  // tuning override: sites per lane (1, 2, 4)
+        const char *e = getenv("SQ_QM1D_K");
+        return e ? atoi(e) : 0;
+    }();
+    if (kforce == 1 || kforce == 2 || kforce == 4) {
+        K = kforce;
+        W = (N + 64 * K - 1) / (64 * K);
+        if (W <= 16) return true;
+    }
+    // measured (profiles/r01/bench_qm1d_wave.log): a lone wave costs about
+    // 1.0 us + 0.47 us per site per lane per step, a multi-wave block ~0.75 us
+    // more for its two barriers
+    if (N <= 128) W = 1;
+    else if (N <= 256) W = (N + 63) / 64;
+    else W = std::min(16, (N + 255) / 256);
+    for (K = 1; 64 * W * K < N; K *= 2) {}
+    return K <= 4;
+}
+
+template <int K>
+static void launch_wave(const Qm1dArgs &a, int W, hipStream_t s) {
+    if (W == 1) hipLaunchKernelGGL((qm1d_frame_wave<K, false>), dim3(1), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((qm1d_frame_wave<K, true>), dim3(1), dim3(64 * W), 0, s, a);
+}
+
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
-    const int K = qm1d_sites_per_thread(a.N);
+    int K = 0, W = 0;
+    if (qm1d_wave_shape(a.N, K, W)) {
+        switch (K) {
+        case 1: launch_wave<1>(a, W, s); break;
+        case 2: launch_wave<2>(a, W, s); break;
+        default: launch_wave<4>(a, W, s); break;
+        }
+        return hipGetLastError();
+    }
+    K = qm1d_sites_per_thread(a.N);
     if (K == 0) return hipErrorInvalidValue;
     int threads = (a.N + K - 1) / K;
     threads = ((threads + 63) / 64) * 64;
     switch (K) {
-    case 1: hipLaunchKernelGGL(qm1d_frame_kernel<1>, dim3(1), dim3(threads), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(qm1d_frame_kernel<2>, dim3(1), dim3(threads), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(qm1d_frame_kernel<4>, dim3(1), dim3(threads), 0, s, a); break;
-    case 8: hipLaunchKernelGGL(qm1d_frame_kernel<8>, dim3(1), dim3(threads), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(qm1d_frame_kernel_glob<8>, dim3(1), dim3(threads), 0, s, a); break;
     case 16: hipLaunchKernelGGL(qm1d_frame_kernel_glob<16>, dim3(1), dim3(threads), 0, s, a); break;
     case 32: hipLaunchKernelGGL(qm1d_frame_kernel_glob<32>, dim3(1), dim3(threads), 0, s, a); break;
     default: hipLaunchKernelGGL(qm1d_frame_kernel_glob<64>, dim3(1), dim3(threads), 0, s, a); break;

@@ -39,6 +39,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "sq_dpp.h"
 #include "sq_internal.h"
 
 namespace sq {
@@ -341,50 +342,6 @@ __global__ __launch_bounds__(256) void gs_xcl_kernel(const Qm1dGsArgs A) {
         A.xc[n + k] = ddpot(x, 3);
     }
 }
-
-// ------------------------------------------------------------- DPP ----
-// Wave-wide max-scans by DPP (row_shr 1/2/4/8, row_bcast 15/31: the gfx9
-// inclusive-scan sequence), no LDS round trips; 64-bit values move as two
-// 32-bit DPP halves.  Out-of-range lanes read the identity (bound_ctrl off).
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ double dpp_d(double v, double id) {
-    const int lo = __builtin_amdgcn_update_dpp((int)__double2loint(id), (int)__double2loint(v), CTRL, RM, BM, false);
-    const int hi = __builtin_amdgcn_update_dpp((int)__double2hiint(id), (int)__double2hiint(v), CTRL, RM, BM, false);
-    return __hiloint2double(hi, lo);
-}
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ int dpp_i(int v, int id) {
-    return __builtin_amdgcn_update_dpp(id, v, CTRL, RM, BM, false);
-}
-__device__ __forceinline__ double dpp_incl_max(double v) {
-    const double id = -__builtin_inf();
-    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x114, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x118, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v, id));
-    return v;
-}
-__device__ __forceinline__ double dpp_excl_max(double v) {  // max over lanes < this lane
-    return dpp_d<0x138, 0xf, 0xf>(dpp_incl_max(v), -__builtin_inf());  // wave_shr:1
-}
-__device__ __forceinline__ double dpp_all_max(double v) {
-    const double s = dpp_incl_max(v);
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(s), 63),
-                            __builtin_amdgcn_readlane(__double2loint(s), 63));
-}
-__device__ __forceinline__ int dpp_all_max_i(int v) {
-    const int id = (int)0x80000000;
-    v = max(v, dpp_i<0x111, 0xf, 0xf>(v, id));
-    v = max(v, dpp_i<0x112, 0xf, 0xf>(v, id));
-    v = max(v, dpp_i<0x114, 0xf, 0xf>(v, id));
-    v = max(v, dpp_i<0x118, 0xf, 0xf>(v, id));
-    v = max(v, dpp_i<0x142, 0xa, 0xf>(v, id));
-    v = max(v, dpp_i<0x143, 0xc, 0xf>(v, id));
-    return __builtin_amdgcn_readlane(v, 63);
-}
-__device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
 
 // ---------------------------------------------------- sweep -> scan ----
 // The sweep and the scan of a frame run concurrently, as two blocks of one
@@ -957,10 +914,6 @@ __device__ __forceinline__ double *gs_rowmax(const Qm1dGsArgs &A) {
     return (double *)(gs_nslot(A) + ((A.loops + 1) & ~1));
 }
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
-                            __builtin_amdgcn_readlane(__double2loint(v), l));
-}
 
 struct GsEval {
     int ll;       // last leader of the step (-1: none)
