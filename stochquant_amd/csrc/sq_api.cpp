@@ -132,6 +132,15 @@ struct sq_ctx {
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;
+    // persistent multi-step launches (single periodic slab; SQ_PERSIST=1: on)
+    int pblocks = 0;                // co-resident blocks of the persistent kernel (0: per-step launches)
+    int pchunk = 500;               // max steps per persistent launch (SQ_PERSIST_STEPS)
+    unsigned int *pdone = nullptr;  // per-unit completion stamps
+    size_t pdone_bytes = 0;
+    int *perr = nullptr;            // a dependency wait timed out
+    unsigned int pstamp = 0;        // stamp of the last completed step
+    bool ppending = false;          // a persistent launch since the last error check
+    long long ev_extra_steps = 0;   // profiling mode 1: steps beyond the first in timed launches
     ncclComm_t comm = nullptr;
     // profiling: 0 off, 1 per launch (hipExtLaunchKernel dispatch timestamps),
     // 2 one event pair around every sq_step call on the step-kernel stream
@@ -154,6 +163,8 @@ int flush_events(sq_ctx *c) {
         c->perf.step_kernel_ms += ms;
         c->perf.step_kernel_launches += 1;
     }
+    c->perf.step_kernel_launches += c->ev_extra_steps;
+    c->ev_extra_steps = 0;
     if (c->region_steps > 0) {  // region mode: one pair per sq_step call covering its steps
         c->perf.step_kernel_launches += c->region_steps - (long long)c->ev_used;
         c->region_steps = 0;
@@ -249,6 +260,52 @@ void count_step(sq_ctx *c) {
     c->step += 1;
     c->perf.steps += 1;
     for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane_floats(c);
+}
+
+// Single slab covering the lattice, all n steps in persistent launches of
+// <= pchunk equal steps (sq_phi4.hip, phi4_persist_kernel).
+int phi4_persist_steps(sq_ctx *c, int n) {
+    Slab &s = c->slabs[0];
+    const int nzc = (s.nz + c->zc - 1) / c->zc;
+    const int nl = (n + c->pchunk - 1) / c->pchunk;
+    for (int l = 0; l < nl; ++l) {
+        const int m = n / nl + (l < n % nl ? 1 : 0);
+        if (c->pstamp > (1u << 30)) {  // stamps wrap-compare; restart them long before 2^31
+            SQ_HIP(hipMemsetAsync(c->pdone, 0, c->pdone_bytes, s.sA));
+            c->pstamp = 0;
+        }
+        sq::Phi4PersistArgs P{};
+        P.a = phi4_base_args(c, s, c->cur);
+        P.a.zlo = 0;
+        P.a.zhi = s.nz;
+        P.a.zstep = c->zc;
+        P.a.zc = c->zc;
+        P.a.nzc = nzc;
+        P.a.periodic = 1;
+        sq::phi4_fill_units(P.a, c->geom);
+        P.buf[0] = s.buf[0];
+        P.buf[1] = s.buf[1];
+        P.done = c->pdone;
+        P.err = c->perr;
+        P.base = c->pstamp;
+        P.cur = c->cur;
+        P.nsteps = m;
+        P.ux = P.a.nunits / 8;
+        EvPair *e = nullptr;
+        if (c->profiling == 1) {
+            int rc = ev_take(c, &e);
+            if (rc) return rc;
+            SQ_HIP(hipEventRecord(e->a, s.sA));
+            c->ev_extra_steps += m - 1;
+        }
+        SQ_HIP(sq::phi4_persist_launch(P, c->geom, c->pblocks, s.sA));
+        if (e) SQ_HIP(hipEventRecord(e->b, s.sA));
+        c->pstamp += (unsigned)m;
+        c->ppending = true;
+        c->cur ^= m & 1;
+        for (int i = 0; i < m; ++i) count_step(c);
+    }
+    return SQ_OK;
 }
 
 // Single slab covering the lattice: one launch per step, z wraps in-kernel.
@@ -428,6 +485,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
 
 int phi4_steps(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
+        if (c->pblocks > 0) return n > 0 ? phi4_persist_steps(c, n) : SQ_OK;
         for (int i = 0; i < n; ++i) {
             int rc = phi4_periodic_step(c);
             if (rc) return rc;
@@ -451,6 +509,12 @@ int phi4_join(sq_ctx *c) {
     for (auto &s : c->slabs) {
         SQ_HIP(hipStreamSynchronize(s.sA));
         SQ_HIP(hipStreamSynchronize(s.sB));
+    }
+    if (c->ppending) {
+        c->ppending = false;
+        int e = 0;
+        SQ_HIP(hipMemcpy(&e, c->perr, sizeof(int), hipMemcpyDeviceToHost));
+        if (e) return fail(SQ_E_HIP, "persistent step kernel: a dependency wait timed out");
     }
     return SQ_OK;
 }
@@ -580,6 +644,27 @@ int create_phi4(sq_ctx *c) {
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
     c->zc = zc;
+    // Opt-in (SQ_PERSIST=1): bit-identical, but measured 46.6 us per 256^3
+    // step vs 21.0 us for per-step launches (profiles/r01/persist_ab.log).
+    const char *pe = getenv("SQ_PERSIST");
+    if (p.comm == SQ_COMM_NONE && pe && atoi(pe) != 0) {
+        const int nxseg = c->Lx / (4 * c->geom.qx * c->geom.v);
+        const long long nunits = (long long)nxseg * ((c->Ly + c->geom.wy - 1) / c->geom.wy) *
+                                 ((c->slabs[0].nz + zc - 1) / zc);
+        int ncu = 0;
+        SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
+        const int blocks = sq::phi4_persist_blocks(c->geom, nxseg > 1, true, ncu);
+        if (blocks >= 8 && nunits % 8 == 0 && nunits < (1ll << 30)) {
+            // no more waves than units: round the block count up to the XCD multiple
+            c->pblocks = (int)std::min<long long>(blocks, ((nunits + 3) / 4 + 7) & ~7ll);
+            c->pdone_bytes = sizeof(unsigned int) * (size_t)nunits;
+            SQ_HIP(hipMalloc(&c->pdone, c->pdone_bytes));
+            SQ_HIP(hipMemset(c->pdone, 0, c->pdone_bytes));
+            SQ_HIP(hipMalloc(&c->perr, sizeof(int)));
+            SQ_HIP(hipMemset(c->perr, 0, sizeof(int)));
+            if (const char *e = getenv("SQ_PERSIST_STEPS")) c->pchunk = std::max(1, atoi(e));
+        }
+    }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
 }
@@ -937,6 +1022,8 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->dacc);
     (void)hipFree(c->dtune);
     (void)hipFree(c->dmax);
+    (void)hipFree(c->pdone);
+    (void)hipFree(c->perr);
     if (c->qstream) (void)hipStreamDestroy(c->qstream);
     for (auto &e : c->evpool) {
         (void)hipEventDestroy(e.a);
@@ -1113,8 +1200,13 @@ int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
     if (pf == 2 && !(c->geom.qx == 64 && c->geom.v == 1)) pf = 1;
     if (pf >= 3 && c->geom.qx != 64) pf = 1;
     if (pf == 5 && ms) pf = 3;
-    snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d> zc=%d", c->geom.qx, c->geom.r, c->geom.v,
-             ms ? "true" : "false", nz ? "true" : "false", pf, c->zc);
+    if (c->pblocks > 0)
+        snprintf(name, cap, "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks",
+                 c->geom.qx, c->geom.r, c->geom.v, ms ? "true" : "false", nz ? "true" : "false", c->zc, c->pchunk,
+                 c->pblocks);
+    else
+        snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d> zc=%d", c->geom.qx, c->geom.r, c->geom.v,
+                 ms ? "true" : "false", nz ? "true" : "false", pf, c->zc);
     return SQ_OK;
 }
 

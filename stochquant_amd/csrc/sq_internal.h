@@ -43,6 +43,23 @@ struct Phi4Geom {
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 
+// Persistent multi-step launch (single periodic slab): every wave owns a fixed
+// set of units and runs them step after step, starting a unit as soon as the
+// units it reads have completed the previous step (dataflow, no kernel
+// boundary between steps).
+struct Phi4PersistArgs {
+    Phi4StepArgs a;       // geometry and physics; a.in / a.out are set per step
+    float *buf[2];        // padded ping-pong; step s reads buf[(cur + s) & 1]
+    unsigned int *done;   // per unit: stamp of its last completed step
+    int *err;             // set to 1 when a dependency wait timed out
+    unsigned int base;    // stamp of the last step completed before this launch
+    int cur, nsteps, ux;  // first input buffer, steps, units per XCD region (nunits / 8)
+};
+// Blocks of the persistent launch for this geometry (all co-resident,
+// multiple of 8), 0 if it has no persistent variant.
+int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu);
+hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s);
+
 // Picks the register tile for (Lx, Ly); returns false if unsupported.
 bool phi4_geometry(int Lx, int Ly, Phi4Geom *g);
 // Fills the work decomposition of a launch that updates `nzc` chunks.

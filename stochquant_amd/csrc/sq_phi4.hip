@@ -19,6 +19,8 @@
 // halo rows and chunk-boundary planes they share hit that XCD's L2.
 #include <hip/hip_ext.h>
 
+#include <algorithm>
+
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -43,8 +45,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, 
     return __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)padded * plane), (short)0,
                                              (int)pbytes, 0x00020000);
 }
+template <int LAUX = 0>
 __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LAUX);
     return make_float4(v.x, v.y, v.z, v.w);
 }
 template <int AUX = 0>
@@ -52,8 +55,9 @@ __device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, 
     const f32x4v w = {v.x, v.y, v.z, v.w};
     __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
 }
+template <int LAUX = 0>
 __device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, LAUX));
 }
 
 __device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
@@ -158,18 +162,18 @@ struct Lane {
     float4 *lds;            // LH: the block's boundary-row exchange buffer
 };
 
-template <int QX, int R, int V>
+template <int QX, int R, int V, int LAUX = 0>
 __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                           Slot<R, V> &s, int zl, bool halo, size_t plane,
                                           uint32_t pbytes) {
     const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, zl), plane, pbytes);
 #pragma unroll
-    for (int k = 0; k < R * V; ++k) s.row[k] = bload4(rs, L.voff[k]);
+    for (int k = 0; k < R * V; ++k) s.row[k] = bload4<LAUX>(rs, L.voff[k]);
     if (halo) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-            if (L.hmask & 1) s.hm[v] = bload4(rs, L.vm[v]);
-            if (L.hmask & 2) s.hp[v] = bload4(rs, L.vp[v]);
+            if (L.hmask & 1) s.hm[v] = bload4<LAUX>(rs, L.vm[v]);
+            if (L.hmask & 2) s.hp[v] = bload4<LAUX>(rs, L.vp[v]);
         }
     }
 }
@@ -178,7 +182,7 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false, int LAUX = 0>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
@@ -190,8 +194,8 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         for (int r = 0; r < R; ++r) {
             el[r] = 0.f;
             er[r] = 0.f;
-            if (L.lane == 0) el[r] = bload1(rs, L.vl[r]);
-            if (L.lane == 63) er[r] = bload1(rs, L.vr[r]);
+            if (L.lane == 0) el[r] = bload1<LAUX>(rs, L.vl[r]);
+            if (L.lane == 63) er[r] = bload1<LAUX>(rs, L.vr[r]);
         }
     }
     // noise for the R*V float4s of plane z: independent of the loads in flight
@@ -293,13 +297,13 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false, int LAUX = 0>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
                                            uint32_t qplane, int &bad) {
-    load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    load_slot<QX, R, V, LAUX>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
@@ -313,14 +317,14 @@ __device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX
     plane_compute<QX, R, V, MS, NZ, false>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
 }
 
-template <int QX, int R, int V, bool MS, bool NZ, int PF>
-__global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
+// One wave's unit of a step: an x-span of 4*QX*V sites by R row sets by a
+// z-chunk.  LAUX: cache policy of the field loads (16 = sc1 in the
+// persistent kernel, whose inputs were written by other waves of the same
+// launch: sc1 loads skip the per-CU L1, which other CUs' stores never
+// refresh).
+template <int QX, int R, int V, bool MS, bool NZ, int PF, int LAUX = 0>
+__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4 *lds, int &bad) {
     constexpr int RS = 64 / QX;  // row sets per wave
-    const int nb = gridDim.x, b = blockIdx.x;
-    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
-    // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
-    const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    if (unit >= A.nunits) return;
     // x-segments fastest, then y-groups: the waves that share a row's segment
     // edges (MS) and the y-halo rows are consecutive units, i.e. the same or
     // the adjacent block on the same XCD, so those lines are L2 hits
@@ -339,8 +343,7 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     L.lane = threadIdx.x & 63;
     L.w = (int)(threadIdx.x >> 6);
     constexpr bool LH = PF == 5;
-    __shared__ float4 s_halo[LH ? 2 * 4 * 2 * V * 64 : 1];
-    L.lds = s_halo;
+    L.lds = lds;
     L.hmask = LH ? ((L.w == 0 ? 1 : 0) | (L.w == 3 ? 2 : 0)) : 3;
     const int xq = L.lane & (QX - 1);
     const int rsid = L.lane / QX;
@@ -374,9 +377,9 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     }
 
     Slot<R, V> S0, S1, S2;
-    load_slot<QX, R, V>(A, L, S0, zbeg - 1, false, plane, pbytes);
-    load_slot<QX, R, V>(A, L, S1, zbeg, true, plane, pbytes);
-    int bad = 0;
+    load_slot<QX, R, V, LAUX>(A, L, S0, zbeg - 1, false, plane, pbytes);
+    load_slot<QX, R, V, LAUX>(A, L, S1, zbeg, true, plane, pbytes);
+    int ubad = 0;
     if constexpr (PF != 2) {
         // three-slot register queue, unrolled so no rotation moves are needed
         // (PF == 3: same queue, packed-f32 site arithmetic)
@@ -391,29 +394,114 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
         // the output does not evict the input rows other waves re-read
         constexpr int SAUX = PF == 4 ? 2 : PF == 6 ? 16 : PF == 7 ? 17 : 0;
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, ubad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, ubad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, ubad);
         }
     } else {
         // four-slot queue, prefetch distance 2
         Slot<R, V> S3;
         load_slot<QX, R, V>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
         for (int z = zbeg; z < zend; z += 4) {
-            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, ubad);
             if (z + 1 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, ubad);
             if (z + 2 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, ubad);
             if (z + 3 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, bad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, ubad);
         }
     }
-    if (!L.rows_ok) bad = 0;
+    if (L.rows_ok) bad |= ubad;
+}
+
+template <int QX, int R, int V, bool MS, bool NZ, int PF>
+__global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
+    const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
+    if (unit >= A.nunits) return;
+    constexpr bool LH = PF == 5;
+    __shared__ float4 s_halo[LH ? 2 * 4 * 2 * V * 64 : 1];
+    int bad = 0;
+    unit_run<QX, R, V, MS, NZ, PF>(A, unit, s_halo, bad);
     if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && L.lane == 0) atomicOr(A.flag, 1);
+        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    }
+}
+
+// ------------------------------------------------------------ persistent ----
+// All steps of an sq_step call in one launch.  Wave k of XCD region x (block
+// b runs on XCD b % 8) runs, every step, the units x*ux + k, x*ux + k + wx,
+// ... (wx waves per region), so each XCD keeps the same contiguous slab of
+// units -- and its halo rows -- step after step.  A unit of step s waits until
+// the 3 x 3 (x 3 with several x-spans) units around it, the only ones whose
+// planes and rows it reads and the only ones that read the planes it
+// overwrites, have completed step s-1; every dependency is on an earlier
+// unit index of the same or earlier step, so with all waves resident
+// (cooperative launch) the smallest unfinished unit can always run.
+// Hand-off (MI355X_MICROARCH.md "Valid forms"): the field is stored with
+// sc0 sc1 (write-through) stores, each wave waits for its stores
+// (vmcnt(0)) before one lane stamps done[unit] (agent-scope store); the
+// consumer polls the stamps with agent-scope loads and reads the field with
+// sc1 loads only, which never hit the per-CU L1.
+constexpr int kPersistSpin = 1 << 21;  // polls before a wait is declared stuck (~seconds)
+
+__device__ __forceinline__ bool wait_deps(const Phi4PersistArgs &P, int unit, unsigned need) {
+    const Phi4StepArgs &A = P.a;
+    const int lane = threadIdx.x & 63;
+    int dep = unit;
+    if (lane < 27) {
+        const int xs = unit % A.nxseg, rest = unit / A.nxseg, yg = rest % A.nyg, zk = rest / A.nyg;
+        int nx = xs + lane % 3 - 1, ny = yg + (lane / 3) % 3 - 1, nzk = zk + lane / 9 - 1;
+        nx = nx < 0 ? A.nxseg - 1 : (nx >= A.nxseg ? 0 : nx);
+        ny = ny < 0 ? A.nyg - 1 : (ny >= A.nyg ? 0 : ny);
+        nzk = nzk < 0 ? A.nzc - 1 : (nzk >= A.nzc ? 0 : nzk);
+        dep = (nzk * A.nyg + ny) * A.nxseg + nx;
+    }
+    for (int it = 0; it < kPersistSpin; ++it) {
+        const unsigned v = __hip_atomic_load(&P.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__ballot((int)(v - need) < 0) == 0ull) {
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no field load moves above the poll
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return false;
+}
+
+template <int QX, int R, int V, bool MS, bool NZ>
+__global__ __launch_bounds__(256) void phi4_persist_kernel(const Phi4PersistArgs P) {
+    const int b = blockIdx.x, x = b & 7;
+    const int wx = (int)(gridDim.x >> 3) * 4;
+    const int k = __builtin_amdgcn_readfirstlane((b >> 3) * 4 + (int)(threadIdx.x >> 6));
+    Phi4StepArgs A = P.a;
+    const unsigned long long s0 = ((unsigned long long)P.a.s_hi << 32) | P.a.s_lo;
+    int bad = 0;
+    for (int s = 0; s < P.nsteps; ++s) {
+        A.in = P.buf[(P.cur + s) & 1];
+        A.out = P.buf[(P.cur + s + 1) & 1];
+        const unsigned long long st = s0 + (unsigned long long)s;
+        A.s_lo = (uint32_t)st;
+        A.s_hi = (uint32_t)(st >> 32);
+        for (int j = k; j < P.ux; j += wx) {
+            const int unit = x * P.ux + j;
+            if (s > 0 && !wait_deps(P, unit, P.base + (unsigned)s)) {
+                if ((threadIdx.x & 63) == 0) atomicOr(P.err, 1);
+                return;  // the waves waiting on this one time out in turn: the grid drains
+            }
+            unit_run<QX, R, V, MS, NZ, 7, 16>(A, unit, nullptr, bad);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store(&P.done[unit], P.base + (unsigned)s + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (A.flag != nullptr) {
+        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     }
 }
 
@@ -611,6 +699,41 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
     case 2: return launch_r<2, 1, false>(a, g, grid, s, e0, e1);
     default: return hipErrorInvalidValue;
     }
+}
+
+// The persistent variants built: the default full-row tiles (R = 1, V = 1 for
+// 256-wide rows; R = 2, V = 2 for rows that are multiples of 512).
+static const void *persist_fn(const Phi4Geom &g, bool ms, bool nz) {
+    if (g.qx != 64) return nullptr;
+    if (g.r == 1 && g.v == 1 && !ms)
+        return nz ? (const void *)&phi4_persist_kernel<64, 1, 1, false, true>
+                  : (const void *)&phi4_persist_kernel<64, 1, 1, false, false>;
+    if (g.r == 2 && g.v == 2)
+        return ms ? (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, true, true>
+                        : (const void *)&phi4_persist_kernel<64, 2, 2, true, false>)
+                  : (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, false, true>
+                        : (const void *)&phi4_persist_kernel<64, 2, 2, false, false>);
+    return nullptr;
+}
+
+int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu) {
+    const void *fn = persist_fn(g, ms, nz);
+    if (fn == nullptr || g.pf != 7) return 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess) return 0;
+    // The occupancy API reads one block per CU high at 97-112 SGPRs
+    // (MI355X_MICROARCH.md, pitfall table): these kernels use 94-106, so cap
+    // at floor(800 / (112 + 16)) = 6 waves per SIMD, i.e. 6 blocks per CU.
+    per_cu = std::min(per_cu, 6);
+    return (per_cu * ncu) & ~7;
+}
+
+hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s) {
+    const void *fn = persist_fn(g, p.a.nxseg > 1, p.a.sig != 0.0f);
+    if (fn == nullptr || blocks <= 0 || (blocks & 7)) return hipErrorInvalidValue;
+    Phi4PersistArgs q = p;
+    void *args[] = {&q};
+    return hipLaunchCooperativeKernel(fn, dim3((unsigned)blocks), dim3(256), args, 0, s);
 }
 
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,

@@ -252,6 +252,73 @@ def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
 
 
+PERSIST_SHAPES = [(256, 8, 8), (256, 16, 12), (256, 32, 33), (512, 4, 8), (512, 8, 12), (1024, 2, 16),
+                  (256, 64, 64)]
+
+
+@pytest.mark.parametrize("shape", PERSIST_SHAPES)
+@pytest.mark.parametrize("C", [0.0, 1.0])
+def test_persistent_launch_bitwise(gpu, oracle_mod, monkeypatch, shape, C):
+    """All steps of an sq_step call in one cooperative launch (units wait on
+    their 27 neighbours' completion stamps of the previous step) == one launch
+    per step, bit for bit, across launch chunks (SQ_PERSIST_STEPS=5) and
+    sq_step calls of odd lengths."""
+    phi0 = _init(oracle_mod, shape)
+    monkeypatch.setenv("SQ_PERSIST", "0")
+    with _lat(shape, C=C) as L:
+        assert "persist" not in L.kernel_name
+        L.upload(phi0)
+        L.step(23)
+        ref = L.download()
+    monkeypatch.setenv("SQ_PERSIST", "1")
+    monkeypatch.setenv("SQ_PERSIST_STEPS", "5")
+    with _lat(shape, C=C) as L:
+        assert "persist" in L.kernel_name, L.kernel_name
+        L.upload(phi0)
+        for n in (1, 3, 12, 7):
+            L.step(n)
+        got = L.download()
+        assert L.step_counter == 23
+    assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+    if C == 0.0:
+        assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 23, C=0.0))
+
+
+def test_persistent_full_size_256(gpu, oracle_mod, monkeypatch):
+    """C2 at full size: 40 steps in persistent launches == per-step launches."""
+    shape = (256, 256, 256)
+    phi0 = _init(oracle_mod, shape, amp=0.5)
+    outs = []
+    for pe in ("0", "1"):
+        monkeypatch.setenv("SQ_PERSIST", pe)
+        with _lat(shape, dtau=0.01, m2=1.0, lam=1.0) as L:
+            assert ("persist" in L.kernel_name) == (pe == "1")
+            L.upload(phi0)
+            L.step(40)
+            outs.append(L.download())
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_persistent_guard_and_rollback(gpu, oracle_mod, monkeypatch):
+    """The clamp / NaN flag raised inside a persistent launch rolls the frame back."""
+    monkeypatch.setenv("SQ_PERSIST", "1")
+    shape = (256, 8, 8)
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    phi0[3, 4, 5] = np.float32(5e3)
+    phi0[6, 1, 130] = np.float32("nan")
+    with _lat(shape, C=0.0, loops=3) as L:
+        assert "persist" in L.kernel_name
+        L.upload(phi0)
+        L.step(1)
+        assert np.array_equal(L.download(), _oracle_run(oracle_mod, shape, phi0, 1, C=0.0))
+    with _lat(shape, loops=3) as L:
+        L.upload(phi0)
+        assert not L.run_frame()
+        back = L.download()
+        assert np.array_equal(back[~np.isnan(phi0)], phi0[~np.isnan(phi0)])
+        assert np.isnan(back[6, 1, 130])
+
+
 @pytest.mark.parametrize("shape", [(512, 4, 6), (1024, 2, 5), (512, 8, 9)])
 @pytest.mark.parametrize("vseg", [1, 2])
 def test_segments_per_lane_bitwise(gpu, oracle_mod, monkeypatch, shape, vseg):
