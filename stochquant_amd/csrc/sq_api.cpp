@@ -134,6 +134,7 @@ struct sq_ctx {
     unsigned int *dmax = nullptr;
     // persistent multi-step launches (single periodic slab; SQ_PERSIST=1: on)
     int pblocks = 0;                // co-resident blocks of the persistent kernel (0: per-step launches)
+    int pU = 1;                     // units per wave per step (pblocks * 4 * pU = units)
     int pchunk = 500;               // max steps per persistent launch (SQ_PERSIST_STEPS)
     unsigned int *pdone = nullptr;  // per-unit completion stamps
     size_t pdone_bytes = 0;
@@ -275,22 +276,23 @@ int phi4_persist_steps(sq_ctx *c, int n) {
             c->pstamp = 0;
         }
         sq::Phi4PersistArgs P{};
-        P.a = phi4_base_args(c, s, c->cur);
-        P.a.zlo = 0;
-        P.a.zhi = s.nz;
-        P.a.zstep = c->zc;
-        P.a.zc = c->zc;
-        P.a.nzc = nzc;
-        P.a.periodic = 1;
-        sq::phi4_fill_units(P.a, c->geom);
-        P.buf[0] = s.buf[0];
-        P.buf[1] = s.buf[1];
+        P.a[0] = phi4_base_args(c, s, c->cur);
+        P.a[0].zlo = 0;
+        P.a[0].zhi = s.nz;
+        P.a[0].zstep = c->zc;
+        P.a[0].zc = c->zc;
+        P.a[0].nzc = nzc;
+        P.a[0].periodic = 1;
+        sq::phi4_fill_units(P.a[0], c->geom);
+        P.a[1] = P.a[0];
+        P.a[1].in = P.a[0].out;
+        P.a[1].out = const_cast<float *>(P.a[0].in);
         P.done = c->pdone;
         P.err = c->perr;
         P.base = c->pstamp;
-        P.cur = c->cur;
         P.nsteps = m;
-        P.ux = P.a.nunits / 8;
+        P.U = c->pU;
+        P.nzq = nzc / c->pU;
         EvPair *e = nullptr;
         if (c->profiling == 1) {
             int rc = ev_take(c, &e);
@@ -644,19 +646,27 @@ int create_phi4(sq_ctx *c) {
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
     c->zc = zc;
-    // Opt-in (SQ_PERSIST=1): bit-identical, but measured 46.6 us per 256^3
-    // step vs 21.0 us for per-step launches (profiles/r01/persist_ab.log).
+    // Opt-in (SQ_PERSIST=1): bit-identical, but measured 55 us per 256^3 step
+    // (31 us with the dependency waits removed) vs 21.5 us for per-step
+    // launches (profiles/r01/persist_ab.log).
     const char *pe = getenv("SQ_PERSIST");
     if (p.comm == SQ_COMM_NONE && pe && atoi(pe) != 0) {
         const int nxseg = c->Lx / (4 * c->geom.qx * c->geom.v);
-        const long long nunits = (long long)nxseg * ((c->Ly + c->geom.wy - 1) / c->geom.wy) *
-                                 ((c->slabs[0].nz + zc - 1) / zc);
+        const int nzc = (c->slabs[0].nz + zc - 1) / zc;
+        const long long nunits = (long long)nxseg * ((c->Ly + c->geom.wy - 1) / c->geom.wy) * nzc;
         int ncu = 0;
         SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
-        const int blocks = sq::phi4_persist_blocks(c->geom, nxseg > 1, true, ncu);
-        if (blocks >= 8 && nunits % 8 == 0 && nunits < (1ll << 30)) {
-            // no more waves than units: round the block count up to the XCD multiple
-            c->pblocks = (int)std::min<long long>(blocks, ((nunits + 3) / 4 + 7) & ~7ll);
+        const long long cap = 4ll * sq::phi4_persist_blocks(c->geom, nxseg > 1, true, ncu);
+        int umin = 1;
+        if (const char *e = getenv("SQ_PERSIST_U")) umin = std::max(1, atoi(e));
+        // the fewest units per wave (most waves) that fit co-resident, with the
+        // same count for every wave and whole blocks on every XCD
+        int U = 0;
+        for (int u = umin; u <= nzc && U == 0; ++u)
+            if (nzc % u == 0 && (nunits / u) % 32 == 0 && nunits / u <= cap) U = u;
+        if (U > 0 && nunits < (1ll << 30)) {
+            c->pU = U;
+            c->pblocks = (int)(nunits / U / 4);
             c->pdone_bytes = sizeof(unsigned int) * (size_t)nunits;
             SQ_HIP(hipMalloc(&c->pdone, c->pdone_bytes));
             SQ_HIP(hipMemset(c->pdone, 0, c->pdone_bytes));
@@ -1201,9 +1211,10 @@ int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
     if (pf >= 3 && c->geom.qx != 64) pf = 1;
     if (pf == 5 && ms) pf = 3;
     if (c->pblocks > 0)
-        snprintf(name, cap, "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks",
+        snprintf(name, cap,
+                 "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks, %d units per wave",
                  c->geom.qx, c->geom.r, c->geom.v, ms ? "true" : "false", nz ? "true" : "false", c->zc, c->pchunk,
-                 c->pblocks);
+                 c->pblocks, c->pU);
     else
         snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d> zc=%d", c->geom.qx, c->geom.r, c->geom.v,
                  ms ? "true" : "false", nz ? "true" : "false", pf, c->zc);

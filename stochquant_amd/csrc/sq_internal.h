@@ -43,17 +43,17 @@ struct Phi4Geom {
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 
-// Persistent multi-step launch (single periodic slab): every wave owns a fixed
-// set of units and runs them step after step, starting a unit as soon as the
-// units it reads have completed the previous step (dataflow, no kernel
-// boundary between steps).
+// Persistent multi-step launch (single periodic slab): every wave owns U units
+// and runs them step after step, starting a unit as soon as the units it
+// reads have completed the previous step (dataflow, no kernel boundary
+// between steps).
 struct Phi4PersistArgs {
-    Phi4StepArgs a;       // geometry and physics; a.in / a.out are set per step
-    float *buf[2];        // padded ping-pong; step s reads buf[(cur + s) & 1]
+    Phi4StepArgs a[2];    // step s of the launch: a[s & 1] (in / out swapped; a[0].in = the first input)
     unsigned int *done;   // per unit: stamp of its last completed step
     int *err;             // set to 1 when a dependency wait timed out
     unsigned int base;    // stamp of the last step completed before this launch
-    int cur, nsteps, ux;  // first input buffer, steps, units per XCD region (nunits / 8)
+    int nsteps;
+    int U, nzq;           // units per wave (z-chunks nzq = nzc / U apart); waves = nunits / U
 };
 // Blocks of the persistent launch for this geometry (all co-resident,
 // multiple of 8), 0 if it has no persistent variant.

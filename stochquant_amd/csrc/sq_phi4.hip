@@ -186,7 +186,7 @@ template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
-                                              uint32_t pbytes, uint32_t qplane, int &bad) {
+                                              uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
     float el[R], er[R];
     if constexpr (MS) {
         const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, z), plane, pbytes);
@@ -204,7 +204,7 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         u32x4 c[R * V];
         const uint32_t qbase = (uint32_t)global_z(A, z) * qplane;
 #pragma unroll
-        for (int k = 0; k < R * V; ++k) c[k] = u32x4{qbase + L.qoff[k], kStreamField << 24, A.s_lo, A.s_hi};
+        for (int k = 0; k < R * V; ++k) c[k] = u32x4{qbase + L.qoff[k], kStreamField << 24, slo, shi};
         philox_rows<R * V>(c, A.k0, A.k1);
 #pragma unroll
         for (int k = 0; k < R * V; ++k) {
@@ -301,9 +301,9 @@ template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
-                                           uint32_t qplane, int &bad) {
+                                           uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
     load_slot<QX, R, V, LAUX>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
 }
 
 // Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
@@ -312,9 +312,9 @@ template <int QX, int R, int V, bool MS, bool NZ>
 __device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                             const Slot<R, V> &P, const Slot<R, V> &C,
                                             const Slot<R, V> &N, Slot<R, V> &F, int z, int zend,
-                                            size_t plane, uint32_t pbytes, uint32_t qplane, int &bad) {
+                                            size_t plane, uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
     if (z + 2 <= zend) load_slot<QX, R, V>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, false>(A, L, P, C, N, z, plane, pbytes, qplane, bad);
+    plane_compute<QX, R, V, MS, NZ, false>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
 }
 
 // One wave's unit of a step: an x-span of 4*QX*V sites by R row sets by a
@@ -323,7 +323,8 @@ __device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX
 // launch: sc1 loads skip the per-CU L1, which other CUs' stores never
 // refresh).
 template <int QX, int R, int V, bool MS, bool NZ, int PF, int LAUX = 0>
-__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4 *lds, int &bad) {
+__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4 *lds, int &bad, uint32_t slo,
+                                         uint32_t shi) {
     constexpr int RS = 64 / QX;  // row sets per wave
     // x-segments fastest, then y-groups: the waves that share a row's segment
     // edges (MS) and the y-halo rows are consecutive units, i.e. the same or
@@ -394,24 +395,24 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4
         // the output does not evict the input rows other waves re-read
         constexpr int SAUX = PF == 4 ? 2 : PF == 6 ? 16 : PF == 7 ? 17 : 0;
         for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, ubad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, slo, shi, ubad);
             if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, ubad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
             if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, ubad);
+            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
         }
     } else {
         // four-slot queue, prefetch distance 2
         Slot<R, V> S3;
         load_slot<QX, R, V>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
         for (int z = zbeg; z < zend; z += 4) {
-            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, ubad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, slo, shi, ubad);
             if (z + 1 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, ubad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
             if (z + 2 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, ubad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
             if (z + 3 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, ubad);
+            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, slo, shi, ubad);
         }
     }
     if (L.rows_ok) bad |= ubad;
@@ -427,22 +428,29 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     constexpr bool LH = PF == 5;
     __shared__ float4 s_halo[LH ? 2 * 4 * 2 * V * 64 : 1];
     int bad = 0;
-    unit_run<QX, R, V, MS, NZ, PF>(A, unit, s_halo, bad);
+    unit_run<QX, R, V, MS, NZ, PF>(A, unit, s_halo, bad, A.s_lo, A.s_hi);
     if (A.flag != nullptr) {
         if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     }
 }
 
 // ------------------------------------------------------------ persistent ----
-// All steps of an sq_step call in one launch.  Wave k of XCD region x (block
-// b runs on XCD b % 8) runs, every step, the units x*ux + k, x*ux + k + wx,
-// ... (wx waves per region), so each XCD keeps the same contiguous slab of
-// units -- and its halo rows -- step after step.  A unit of step s waits until
-// the 3 x 3 (x 3 with several x-spans) units around it, the only ones whose
-// planes and rows it reads and the only ones that read the planes it
-// overwrites, have completed step s-1; every dependency is on an earlier
-// unit index of the same or earlier step, so with all waves resident
-// (cooperative launch) the smallest unfinished unit can always run.
+// All steps of an sq_step call in one launch.  Every wave owns U units of the
+// same x-span and y-group whose z-chunks are nzq = nzc / U apart (c0, c0 +
+// nzq, ...) and runs them in that order, step after step; every wave has the
+// same U, so no wave is a straggler.  A unit of step s waits until the 3 x 3
+// (x 3 with several x-spans) units around it -- the only ones whose planes and
+// rows it reads, and the only ones that read the planes it overwrites -- have
+// completed step s-1.  Those neighbours (z-chunks c +- 1) are, but for the
+// units at a multiple of nzq, units of the same rank i in their own waves,
+// which ran them while this wave ran its units i+1..U-1 of step s-1 and 0..i-1
+// of step s, so the wait is normally already satisfied.  Deadlock freedom:
+// the (step, rank) pairs are ordered, every dependency is on a smaller pair,
+// and all waves are resident (cooperative launch), so the smallest
+// unfinished unit can always run.
+// XCD locality: block b runs on XCD b % 8 and the waves of XCD x are the
+// consecutive wave ids g in [x WX, (x+1) WX), x-span fastest, then y-group,
+// then c0, so an XCD holds whole planes of y-groups and their halo rows.
 // Hand-off (MI355X_MICROARCH.md "Valid forms"): the field is stored with
 // sc0 sc1 (write-through) stores, each wave waits for its stores
 // (vmcnt(0)) before one lane stamps done[unit] (agent-scope store); the
@@ -450,12 +458,12 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
 // sc1 loads only, which never hit the per-CU L1.
 constexpr int kPersistSpin = 1 << 21;  // polls before a wait is declared stuck (~seconds)
 
-__device__ __forceinline__ bool wait_deps(const Phi4PersistArgs &P, int unit, unsigned need) {
-    const Phi4StepArgs &A = P.a;
+__device__ __forceinline__ bool wait_deps(const Phi4PersistArgs &P, int xs, int yg, int zk, int unit,
+                                          unsigned need) {
+    const Phi4StepArgs &A = P.a[0];
     const int lane = threadIdx.x & 63;
     int dep = unit;
     if (lane < 27) {
-        const int xs = unit % A.nxseg, rest = unit / A.nxseg, yg = rest % A.nyg, zk = rest / A.nyg;
         int nx = xs + lane % 3 - 1, ny = yg + (lane / 3) % 3 - 1, nzk = zk + lane / 9 - 1;
         nx = nx < 0 ? A.nxseg - 1 : (nx >= A.nxseg ? 0 : nx);
         ny = ny < 0 ? A.nyg - 1 : (ny >= A.nyg ? 0 : ny);
@@ -473,35 +481,54 @@ __device__ __forceinline__ bool wait_deps(const Phi4PersistArgs &P, int unit, un
     return false;
 }
 
+// Step s of a persistent launch: this wave's U units in rank order.  False
+// when a dependency wait timed out (the error is flagged; the wave exits).
+typedef const __attribute__((address_space(4))) Phi4StepArgs *KArgs;
 template <int QX, int R, int V, bool MS, bool NZ>
-__global__ __launch_bounds__(256) void phi4_persist_kernel(const Phi4PersistArgs P) {
-    const int b = blockIdx.x, x = b & 7;
-    const int wx = (int)(gridDim.x >> 3) * 4;
-    const int k = __builtin_amdgcn_readfirstlane((b >> 3) * 4 + (int)(threadIdx.x >> 6));
-    Phi4StepArgs A = P.a;
-    const unsigned long long s0 = ((unsigned long long)P.a.s_hi << 32) | P.a.s_lo;
-    int bad = 0;
-    for (int s = 0; s < P.nsteps; ++s) {
-        A.in = P.buf[(P.cur + s) & 1];
-        A.out = P.buf[(P.cur + s + 1) & 1];
-        const unsigned long long st = s0 + (unsigned long long)s;
-        A.s_lo = (uint32_t)st;
-        A.s_hi = (uint32_t)(st >> 32);
-        for (int j = k; j < P.ux; j += wx) {
-            const int unit = x * P.ux + j;
-            if (s > 0 && !wait_deps(P, unit, P.base + (unsigned)s)) {
-                if ((threadIdx.x & 63) == 0) atomicOr(P.err, 1);
-                return;  // the waves waiting on this one time out in turn: the grid drains
-            }
-            unit_run<QX, R, V, MS, NZ, 7, 16>(A, unit, nullptr, bad);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if ((threadIdx.x & 63) == 0)
-                __hip_atomic_store(&P.done[unit], P.base + (unsigned)s + 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ bool persist_step(const Phi4PersistArgs &P, KArgs pa, int s, unsigned long long s0,
+                                             int xs, int yg, int c0, int &bad) {
+    const unsigned long long st = s0 + (unsigned long long)s;
+    for (int i = 0; i < P.U; ++i) {
+        // the unit's argument block is read from the kernarg segment through a
+        // pointer the compiler cannot see through, so nothing derived from it
+        // is hoisted out of the unit / step loops and held in SGPRs across
+        // iterations (hoisting spilled 41-137 SGPRs)
+        KArgs q = pa;
+        asm volatile("" : "+s"(q));
+        const Phi4StepArgs &A = *(const Phi4StepArgs *)q;
+        const int zk = c0 + i * P.nzq;
+        const int unit = (zk * A.nyg + yg) * A.nxseg + xs;
+        if (s > 0 && !wait_deps(P, xs, yg, zk, unit, P.base + (unsigned)s)) {
+            if ((threadIdx.x & 63) == 0) atomicOr(P.err, 1);
+            return false;  // the waves waiting on this one time out in turn: the grid drains
         }
+        unit_run<QX, R, V, MS, NZ, 7, 16>(A, unit, nullptr, bad, (uint32_t)st, (uint32_t)(st >> 32));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if ((threadIdx.x & 63) == 0)
+            __hip_atomic_store(&P.done[unit], P.base + (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    return true;
+}
+
+// WPE: waves per SIMD the registers are budgeted for (the whole grid must be
+// resident; at 7 the one-row tile keeps its SGPRs at 87-94, under the 97-112
+// band where the occupancy API reads high: MI355X_MICROARCH.md pitfall
+// table; a budget of 8 spilled 60 SGPRs and a VGPR to scratch).
+template <int QX, int R, int V, bool MS, bool NZ, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_persist_kernel(const Phi4PersistArgs P) {
+    const int b = blockIdx.x;
+    const int wxcd = (int)(gridDim.x >> 3) * 4;  // waves per XCD
+    const int g = __builtin_amdgcn_readfirstlane((b & 7) * wxcd + (b >> 3) * 4 + (int)(threadIdx.x >> 6));
+    const int xs = g % P.a[0].nxseg, rest = g / P.a[0].nxseg, yg = rest % P.a[0].nyg, c0 = rest / P.a[0].nyg;
+    const unsigned long long s0 = ((unsigned long long)P.a[0].s_hi << 32) | P.a[0].s_lo;
+    int bad = 0;
+    const KArgs a0 = (KArgs)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
+                             offsetof(Phi4PersistArgs, a));
+    for (int s = 0; s < P.nsteps; ++s) {
+        if (!persist_step<QX, R, V, MS, NZ>(P, a0 + (s & 1), s, s0, xs, yg, c0, bad)) return;
+    }
+    if (P.a[0].flag != nullptr) {
+        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(P.a[0].flag, 1);
     }
 }
 
@@ -706,13 +733,13 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
 static const void *persist_fn(const Phi4Geom &g, bool ms, bool nz) {
     if (g.qx != 64) return nullptr;
     if (g.r == 1 && g.v == 1 && !ms)
-        return nz ? (const void *)&phi4_persist_kernel<64, 1, 1, false, true>
-                  : (const void *)&phi4_persist_kernel<64, 1, 1, false, false>;
+        return nz ? (const void *)&phi4_persist_kernel<64, 1, 1, false, true, 7>
+                  : (const void *)&phi4_persist_kernel<64, 1, 1, false, false, 7>;
     if (g.r == 2 && g.v == 2)
-        return ms ? (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, true, true>
-                        : (const void *)&phi4_persist_kernel<64, 2, 2, true, false>)
-                  : (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, false, true>
-                        : (const void *)&phi4_persist_kernel<64, 2, 2, false, false>);
+        return ms ? (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, true, true, 3>
+                        : (const void *)&phi4_persist_kernel<64, 2, 2, true, false, 3>)
+                  : (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, false, true, 3>
+                        : (const void *)&phi4_persist_kernel<64, 2, 2, false, false, 3>);
     return nullptr;
 }
 
@@ -722,14 +749,14 @@ int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess) return 0;
     // The occupancy API reads one block per CU high at 97-112 SGPRs
-    // (MI355X_MICROARCH.md, pitfall table): these kernels use 94-106, so cap
-    // at floor(800 / (112 + 16)) = 6 waves per SIMD, i.e. 6 blocks per CU.
-    per_cu = std::min(per_cu, 6);
+    // (MI355X_MICROARCH.md, pitfall table): the one-row kernels stay under it
+    // (WPE 7), the two-row ones are VGPR-bound at 3; bound by both anyway.
+    per_cu = std::min(per_cu, g.r == 1 && g.v == 1 ? 7 : 3);
     return (per_cu * ncu) & ~7;
 }
 
 hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s) {
-    const void *fn = persist_fn(g, p.a.nxseg > 1, p.a.sig != 0.0f);
+    const void *fn = persist_fn(g, p.a[0].nxseg > 1, p.a[0].sig != 0.0f);
     if (fn == nullptr || blocks <= 0 || (blocks & 7)) return hipErrorInvalidValue;
     Phi4PersistArgs q = p;
     void *args[] = {&q};

@@ -252,7 +252,9 @@ def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
 
 
-PERSIST_SHAPES = [(256, 8, 8), (256, 16, 12), (256, 32, 33), (512, 4, 8), (512, 8, 12), (1024, 2, 16),
+# unit counts (x-spans * y-groups * z-chunks) that are multiples of 32, so
+# every wave gets the same number of units
+PERSIST_SHAPES = [(256, 8, 8), (256, 16, 12), (256, 32, 33), (512, 8, 16), (512, 16, 12), (1024, 2, 16),
                   (256, 64, 64)]
 
 
@@ -282,6 +284,25 @@ def test_persistent_launch_bitwise(gpu, oracle_mod, monkeypatch, shape, C):
     assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
     if C == 0.0:
         assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 23, C=0.0))
+
+
+@pytest.mark.parametrize("shape,units", [((256, 32, 32), 2), ((256, 32, 32), 4), ((256, 64, 64), 4),
+                                         ((512, 16, 32), 8)])
+def test_persistent_units_per_wave_bitwise(gpu, oracle_mod, monkeypatch, shape, units):
+    """Several units per wave (z-chunks nzc/U apart, run in rank order)."""
+    phi0 = _init(oracle_mod, shape)
+    monkeypatch.setenv("SQ_PERSIST", "0")
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(17)
+        ref = L.download()
+    monkeypatch.setenv("SQ_PERSIST", "1")
+    monkeypatch.setenv("SQ_PERSIST_U", str(units))
+    with _lat(shape) as L:
+        assert f"{units} units per wave" in L.kernel_name, L.kernel_name
+        L.upload(phi0)
+        L.step(17)
+        assert np.array_equal(L.download(), ref)
 
 
 def test_persistent_full_size_256(gpu, oracle_mod, monkeypatch):
