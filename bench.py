@@ -12,9 +12,12 @@ interior planes.
 
 Prints ONE JSON line (rank 0).  `value` = all site updates of all ranks / max
 over ranks of the barrier-bracketed wall time of the K timed steps.
-`roofline.achieved` = 8 algorithmic bytes x sites per launch / mean duration of
-the step-kernel launches in the timed region (hipEvents recorded on the
-kernel's own stream by libstochquant.so).  `cpu_baseline` = the oracle's C port
+`roofline.achieved` = 8 algorithmic bytes per site update x the
+site updates of one launch / mean duration of the launches in the timed
+region (hipEvents recorded on the kernel's own stream by libstochquant.so).
+At N = 1 on 256-wide lattices a launch fuses two steps (phi4_tb2_kernel), so
+it moves the field once per two updates: `hbm_min_GBps` is the rate of that
+one read + one write, `traffic` the PMC-measured bytes per launch.  `cpu_baseline` = the oracle's C port
 of the same step (OpenMP over the box's host cores) on a bounded sample.
 """
 import argparse
@@ -76,7 +79,7 @@ def cpu_baseline(L, dtau, target_s):
                       f"{cores} threads), {dt:.2f} s"}
 
 
-def pmc_traffic(L, nranks):
+def pmc_traffic(L, nranks, kernel):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches this workload."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -84,7 +87,8 @@ def pmc_traffic(L, nranks):
             d = json.load(fh)
     except (OSError, ValueError):
         return None
-    if d.get("size") == L and d.get("nranks", 1) == nranks:
+    same_kernel = ("phi4_tb2_kernel" in d.get("kernel", "")) == ("phi4_tb2_kernel" in kernel)
+    if d.get("size") == L and d.get("nranks", 1) == nranks and same_kernel:
         return d.get("hbm_bytes_per_launch")
     return None
 
@@ -165,7 +169,11 @@ def main():
     else:
         avg_ms = t * 1e3 / a.steps
         sites_per_launch = sites_local
-    achieved = BYTES_PER_SITE * sites_per_launch / (avg_ms * 1e-3) / 1e9
+    # two-step fused launches (phi4_tb2_kernel) update every site twice
+    kname = lat.kernel_name
+    spl = 2 if "2 steps per launch" in kname else 1
+    launch_ms = avg_ms * spl
+    achieved = BYTES_PER_SITE * sites_per_launch * spl / (launch_ms * 1e-3) / 1e9
     out = None
     if rank == 0:
         copy = None
@@ -207,13 +215,19 @@ def main():
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": pmc_traffic(L, world),
-                "kernel": lat.kernel_name,
+                "traffic": pmc_traffic(L, world, kname),
+                "kernel": kname,
                 "timing": "hipEvent pair on the kernel stream around the timed launches (region mean)"
                           if perf["step_kernel_launches"] > 0 else "wall clock",
-                "algorithmic_bytes_per_launch": BYTES_PER_SITE * sites_per_launch,
-                "avg_launch_us": round(avg_ms * 1e3, 3),
-                "launches_timed": perf["step_kernel_launches"],
+                "steps_per_launch": spl,
+                "algorithmic_bytes_per_launch": BYTES_PER_SITE * sites_per_launch * spl,
+                "avg_launch_us": round(launch_ms * 1e3, 3),
+                "avg_step_us": round(avg_ms * 1e3, 3),
+                "launches_timed": perf["step_kernel_launches"] // spl,
+                # the least HBM traffic a launch can have (one read + one write
+                # of the field) and the rate it moved at
+                "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_per_launch,
+                "hbm_min_GBps": round(BYTES_PER_SITE * sites_per_launch / (launch_ms * 1e-3) / 1e9, 1),
             },
             "hbm_copy_peak_GBps": copy,
             "field_check": {"rms": (m["sum2"] / sites_local) ** 0.5, "maxabs": m["maxabs"]},

@@ -1,6 +1,9 @@
 """Turn two rocprofv3 --pmc runs (FETCH_SIZE, WRITE_SIZE; separate passes,
 MI355X_MICROARCH.md §rocprofv3 PMC slots) into HBM bytes per launch of the
-phi^4 step kernel, and write profiles/pmc_traffic.json for bench.py.
+phi^4 step kernel (one step per launch) or two-step fused kernel (two), and
+write profiles/pmc_traffic.json for bench.py.  algorithmic bytes = 8 B per
+site update x the updates of one launch; hbm_min = one read
+and one write of the field, the least any launch can move.
 
 gfx950 corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE (KiB) counts the
 L2's memory-side read requests at 64 B but wide streaming reads issue 128-B
@@ -19,7 +22,7 @@ import os
 import statistics
 
 
-def counter_values(d, counter, kernel_substr="phi4_step_kernel"):
+def counter_values(d, counter, kernel_substr="phi4_"):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -54,7 +57,9 @@ def main():
     write_kib = statistics.median(wv_s)
     read_bytes = 2.0 * fetch_kib * 1024
     write_bytes = write_kib * 1024
-    alg = 8 * a.size ** 3
+    # two-step fused launches (phi4_tb2_kernel) do two site updates per site
+    spl = 2 if "tb2" in kname else 1
+    alg = 8 * a.size ** 3 * spl
     out = {
         "size": a.size,
         "nranks": a.nranks,
@@ -65,8 +70,11 @@ def main():
         "read_bytes_per_launch": read_bytes,
         "write_bytes_per_launch": write_bytes,
         "hbm_bytes_per_launch": read_bytes + write_bytes,
+        "steps_per_launch": spl,
         "algorithmic_bytes_per_launch": alg,
         "traffic_over_algorithmic": (read_bytes + write_bytes) / alg,
+        "hbm_min_bytes_per_launch": 8 * a.size ** 3,
+        "traffic_over_hbm_min": (read_bytes + write_bytes) / (8 * a.size ** 3),
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB x1024",
     }
     with open(a.out, "w") as fh:

@@ -135,6 +135,7 @@ struct sq_ctx {
     // persistent multi-step launches (single periodic slab; SQ_PERSIST=1: on)
     int pblocks = 0;                // co-resident blocks of the persistent kernel (0: per-step launches)
     int pU = 1;                     // units per wave per step (pblocks * 4 * pU = units)
+    int tbz = 0;                    // two-step fused launches: output planes per block (0: off)
     int pchunk = 500;               // max steps per persistent launch (SQ_PERSIST_STEPS)
     unsigned int *pdone = nullptr;  // per-unit completion stamps
     size_t pdone_bytes = 0;
@@ -307,6 +308,33 @@ int phi4_persist_steps(sq_ctx *c, int n) {
         c->cur ^= m & 1;
         for (int i = 0; i < m; ++i) count_step(c);
     }
+    return SQ_OK;
+}
+
+// Single slab covering the lattice: steps s and s+1 in one launch
+// (sq_phi4.hip, phi4_tb2_kernel); the output lands in the other buffer.
+int phi4_tb2_pair(sq_ctx *c) {
+    Slab &s = c->slabs[0];
+    sq::Phi4StepArgs a = phi4_base_args(c, s, c->cur);
+    a.zlo = 0;
+    a.zhi = s.nz;
+    a.zstep = c->tbz;
+    a.zc = c->tbz;
+    a.nzc = (s.nz + c->tbz - 1) / c->tbz;
+    a.periodic = 1;
+    a.nxseg = 1;
+    a.nyg = c->Ly / 8;
+    a.nunits = a.nyg * a.nzc;
+    EvPair *e = nullptr;
+    if (c->profiling == 1) {
+        int rc = ev_take(c, &e);
+        if (rc) return rc;
+        c->ev_extra_steps += 1;
+    }
+    SQ_HIP(sq::phi4_tb2_launch(a, s.sA, e ? e->a : nullptr, e ? e->b : nullptr));
+    c->cur ^= 1;
+    count_step(c);
+    count_step(c);
     return SQ_OK;
 }
 
@@ -488,6 +516,10 @@ int phi4_autotune(sq_ctx *c, int &n) {
 int phi4_steps(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
         if (c->pblocks > 0) return n > 0 ? phi4_persist_steps(c, n) : SQ_OK;
+        for (; c->tbz > 0 && n >= 2; n -= 2) {
+            int rc = phi4_tb2_pair(c);
+            if (rc) return rc;
+        }
         for (int i = 0; i < n; ++i) {
             int rc = phi4_periodic_step(c);
             if (rc) return rc;
@@ -649,6 +681,15 @@ int create_phi4(sq_ctx *c) {
     // Opt-in (SQ_PERSIST=1): bit-identical, but measured 55 us per 256^3 step
     // (31 us with the dependency waits removed) vs 21.5 us for per-step
     // launches (profiles/r01/persist_ab.log).
+    // Two steps per launch on 256-wide single-slab lattices (SQ_FUSE2=0: off;
+    // SQ_FUSE2_Z: output planes per block).  256^3: 19.5 vs 22.0 us per step
+    // on the same box; z = 16 (512 blocks, two per CU) measured best of
+    // 8/11/12/16/22/32 (profiles/r01/fuse2_sweep.log).
+    const char *fe = getenv("SQ_FUSE2");
+    if (!(fe && atoi(fe) == 0) && p.comm == SQ_COMM_NONE && sq::phi4_tb2_supported(c->Lx, c->Ly, c->slabs[0].nz)) {
+        c->tbz = 16;
+        if (const char *z = getenv("SQ_FUSE2_Z")) c->tbz = std::max(1, atoi(z));
+    }
     const char *pe = getenv("SQ_PERSIST");
     if (p.comm == SQ_COMM_NONE && pe && atoi(pe) != 0) {
         const int nxseg = c->Lx / (4 * c->geom.qx * c->geom.v);
@@ -665,6 +706,7 @@ int create_phi4(sq_ctx *c) {
         for (int u = umin; u <= nzc && U == 0; ++u)
             if (nzc % u == 0 && (nunits / u) % 32 == 0 && nunits / u <= cap) U = u;
         if (U > 0 && nunits < (1ll << 30)) {
+            c->tbz = 0;  // the persistent launches replace the two-step fusion
             c->pU = U;
             c->pblocks = (int)(nunits / U / 4);
             c->pdone_bytes = sizeof(unsigned int) * (size_t)nunits;
@@ -1210,7 +1252,9 @@ int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
     if (pf == 2 && !(c->geom.qx == 64 && c->geom.v == 1)) pf = 1;
     if (pf >= 3 && c->geom.qx != 64) pf = 1;
     if (pf == 5 && ms) pf = 3;
-    if (c->pblocks > 0)
+    if (c->tbz > 0)
+        snprintf(name, cap, "phi4_tb2_kernel<%s> (2 steps per launch) z=%d", nz ? "true" : "false", c->tbz);
+    else if (c->pblocks > 0)
         snprintf(name, cap,
                  "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks, %d units per wave",
                  c->geom.qx, c->geom.r, c->geom.v, ms ? "true" : "false", nz ? "true" : "false", c->zc, c->pchunk,

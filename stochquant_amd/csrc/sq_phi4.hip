@@ -532,6 +532,145 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     }
 }
 
+// ----------------------------------------------------- two-step fusion ----
+// Steps s and s+1 in one pass over the field (temporal blocking), for
+// 256-wide rows on a single periodic slab.  A block of kTbWaves = 10 waves
+// owns kTbRows = 8 output rows [y0, y0+8) of a z-chunk [z0, z1); wave w
+// holds row y0-1+w.  Marching p over [z0-1, z1]:
+//   1. every wave loads input plane p+1 (its row and both y-halo rows) and
+//      updates its row of plane p by step s -> T(p) (the same site update,
+//      noise keyed by step s), keeps T in a 3-plane register queue and
+//      publishes it in LDS slot p % 3;
+//   2. barrier;
+//   3. waves 1..8 update their row of plane p-1 by step s+1 from T(p-2),
+//      T(p-1), T(p) (registers) and the y-neighbour rows of T(p-1) (LDS).
+// Rows y0-1, y0+8 and planes z0-1, z1 of T are recomputed by the adjacent
+// blocks too: the counter-based noise makes them bit-identical, so the
+// result equals two single steps bit for bit.  HBM traffic: one read and one
+// write of the field per two steps.  Three LDS slots: a slot is rewritten
+// two barriers after its last reader passed the barrier before its read.
+constexpr int kTbRows = 8;
+constexpr int kTbWaves = kTbRows + 2;
+
+__device__ __forceinline__ int tb_pidx(const Phi4StepArgs &A, int zl) {  // periodic, |overflow| <= 2
+    return (zl < 0 ? zl + A.nz : (zl >= A.nz ? zl - A.nz : zl)) + A.gz;
+}
+
+template <bool NZ>
+__device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, int zl, uint32_t qoff, uint32_t qplane,
+                                           uint32_t slo, uint32_t shi) {
+    f32x4n xi;
+    if constexpr (NZ) {
+        u32x4 c[1];
+        c[0] = u32x4{(uint32_t)global_z(A, zl) * qplane + qoff, kStreamField << 24, slo, shi};
+        philox_rows<1>(c, A.k0, A.k1);
+        box_muller(c[0].x, c[0].y, xi.a, xi.b);
+        box_muller(c[0].z, c[0].w, xi.c, xi.d);
+    } else {
+        xi = f32x4n{0.f, 0.f, 0.f, 0.f};
+    }
+    return xi;
+}
+
+struct TbIn {
+    float4 row, hm, hp;  // the wave's row and its two y-neighbours at one plane
+};
+
+// One plane of the march: see above.  I0 (p-1), I1 (p), I2 (p+1, loaded here);
+// T0 (p-2), T1 (p-1), T2 (p, computed here).
+template <bool NZ>
+__device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, int p, int z0, const TbIn &I0, const TbIn &I1,
+                                         TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
+                                         float4 (*lds)[kTbWaves][64], int w, int lane, bool outw,
+                                         uint32_t voff, uint32_t vm, uint32_t vp, uint32_t qoff, size_t plane,
+                                         uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi,
+                                         uint32_t slo1, uint32_t shi1, int &bad) {
+    {
+        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, tb_pidx(A, p + 1), plane, pbytes);
+        I2.row = bload4(rs, voff);
+        I2.hm = bload4(rs, vm);
+        I2.hp = bload4(rs, vp);
+    }
+    const f32x4n xa = tb_noise<NZ>(A, p, qoff, qplane, slo, shi);
+    f32x4n xb = f32x4n{0.f, 0.f, 0.f, 0.f};
+    const bool doB = outw && p > z0;
+    if (doB) xb = tb_noise<NZ>(A, p - 1, qoff, qplane, slo1, shi1);
+    T2 = site_update4<NZ>(I1.row, from_left_lane(I1.row.w), from_right_lane(I1.row.x), I1.hm, I1.hp, I0.row,
+                          I2.row, xa, A);
+    if (A.flag != nullptr) {
+        const float m = fmaxf(fmaxf(fabsf(T2.x), fabsf(T2.y)), fmaxf(fabsf(T2.z), fabsf(T2.w)));
+        bad |= (int)(m >= A.clampv);
+    }
+    const int sl = p % 3;
+    lds[sl][w][lane] = T2;
+    __syncthreads();
+    if (doB) {
+        const int sp = (p + 2) % 3;  // slot of plane p-1
+        const float4 up = lds[sp][w - 1][lane], dn = lds[sp][w + 1][lane];
+        const float4 o = site_update4<NZ>(T1, from_left_lane(T1.w), from_right_lane(T1.x), up, dn, T0, T2, xb, A);
+        if (A.flag != nullptr) {
+            const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+            bad |= (int)(m >= A.clampv);
+        }
+        const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, plane, pbytes);
+        bstore4<17>(ws, voff, o);
+    }
+}
+
+// 68 VGPRs: two 10-wave blocks per CU.  A 64-VGPR budget (three blocks per
+// CU) measured slower at every z-chunk (profiles/r01/fuse2_sweep.log): the
+// kernel is issue-bound, not latency-bound.
+template <bool NZ>
+__global__ __launch_bounds__(kTbWaves * 64) void phi4_tb2_kernel(const Phi4StepArgs A) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // y-bands of a z-chunk on one XCD
+    const int yb = lb % A.nyg, zk = lb / A.nyg;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63;
+    const int Lx = A.Lx, Ly = A.Ly;
+    int y = yb * kTbRows - 1 + w;
+    y = y < 0 ? y + Ly : (y >= Ly ? y - Ly : y);
+    const int ym = y == 0 ? Ly - 1 : y - 1, yp = y == Ly - 1 ? 0 : y + 1;
+    const uint32_t voff = (uint32_t)((y * Lx + 4 * lane) * 4);
+    const uint32_t vm = (uint32_t)((ym * Lx + 4 * lane) * 4), vp = (uint32_t)((yp * Lx + 4 * lane) * 4);
+    const uint32_t qoff = (uint32_t)((y * Lx + 4 * lane) >> 2);
+    const bool outw = w >= 1 && w <= kTbRows;
+    const int z0 = zk * A.zc, z1 = min(z0 + A.zc, A.nz);
+    const size_t plane = (size_t)Lx * (size_t)Ly;
+    const uint32_t pbytes = (uint32_t)(plane * sizeof(float));
+    const uint32_t qplane = (uint32_t)(plane >> 2);
+    const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
+    const uint32_t slo = (uint32_t)s0, shi = (uint32_t)(s0 >> 32), slo1 = (uint32_t)s1, shi1 = (uint32_t)(s1 >> 32);
+    __shared__ float4 lds[3][kTbWaves][64];
+
+    TbIn I0, I1, I2;
+    {
+        const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, z0 - 2), plane, pbytes);
+        I0.row = bload4(r0, voff);
+        I0.hm = I0.hp = I0.row;
+        const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(A.in, tb_pidx(A, z0 - 1), plane, pbytes);
+        I1.row = bload4(r1, voff);
+        I1.hm = bload4(r1, vm);
+        I1.hp = bload4(r1, vp);
+    }
+    float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
+    int bad = 0;
+    // three-plane queues unrolled three ways so no rotation moves are emitted
+    for (int p = z0 - 1; p <= z1; p += 3) {
+        tb_plane<NZ>(A, p, z0, I0, I1, I2, T0, T1, T2, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
+                     qplane, slo, shi, slo1, shi1, bad);
+        if (p + 1 > z1) break;
+        tb_plane<NZ>(A, p + 1, z0, I1, I2, I0, T1, T2, T0, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
+                     qplane, slo, shi, slo1, shi1, bad);
+        if (p + 2 > z1) break;
+        tb_plane<NZ>(A, p + 2, z0, I2, I0, I1, T2, T0, T1, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
+                     qplane, slo, shi, slo1, shi1, bad);
+    }
+    if (A.flag != nullptr) {
+        if (__ballot(bad) != 0ull && lane == 0) atomicOr(A.flag, 1);
+    }
+}
+
 __global__ __launch_bounds__(256) void phi4_init_kernel(float *slab, int Lx, int Ly, int nz,
                                                         long long zg0, uint32_t k0, uint32_t k1,
                                                         float amp) {
@@ -741,6 +880,18 @@ static const void *persist_fn(const Phi4Geom &g, bool ms, bool nz) {
                   : (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, false, true, 3>
                         : (const void *)&phi4_persist_kernel<64, 2, 2, false, false, 3>);
     return nullptr;
+}
+
+bool phi4_tb2_supported(int Lx, int Ly, int nz) { return Lx == 256 && Ly % kTbRows == 0 && nz >= 2; }
+
+hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (!phi4_tb2_supported(a.Lx, a.Ly, a.nz) || !a.periodic || a.nunits <= 0) return hipErrorInvalidValue;
+    const dim3 grid((unsigned)a.nunits), block(kTbWaves * 64);
+    const void *fn = a.sig != 0.0f ? (const void *)&phi4_tb2_kernel<true> : (const void *)&phi4_tb2_kernel<false>;
+    Phi4StepArgs q = a;
+    void *args[] = {&q};
+    if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
+    return hipLaunchKernel(fn, grid, block, args, 0, s);
 }
 
 int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu) {

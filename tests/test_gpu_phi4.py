@@ -244,6 +244,7 @@ def test_rccl_self_exchange_deep_halo_frames(gpu, oracle_mod, monkeypatch):
 @pytest.mark.parametrize("pf", [1, 2, 3, 4, 5, 6, 7])
 def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     monkeypatch.setenv("SQ_PREFETCH", str(pf))
+    monkeypatch.setenv("SQ_FUSE2", "0")  # every step through the per-step kernel variant
     phi0 = _init(oracle_mod, shape)
     with _lat(shape, C=0.0) as L:
         L.upload(phi0)
@@ -338,6 +339,74 @@ def test_persistent_guard_and_rollback(gpu, oracle_mod, monkeypatch):
         back = L.download()
         assert np.array_equal(back[~np.isnan(phi0)], phi0[~np.isnan(phi0)])
         assert np.isnan(back[6, 1, 130])
+
+
+FUSE2_SHAPES = [(256, 8, 2), (256, 8, 5), (256, 16, 12), (256, 32, 33), (256, 64, 64), (256, 24, 17)]
+
+
+@pytest.mark.parametrize("shape", FUSE2_SHAPES)
+@pytest.mark.parametrize("zb", [1, 3, 16])
+@pytest.mark.parametrize("C", [0.0, 1.0])
+def test_fused_two_step_bitwise(gpu, oracle_mod, monkeypatch, shape, zb, C):
+    """Steps s and s+1 in one launch (8-row y-bands with their halo rows and
+    the chunk-edge planes of step s recomputed per block) == two single-step
+    launches, bit for bit; odd step counts end with one single step."""
+    phi0 = _init(oracle_mod, shape)
+    monkeypatch.setenv("SQ_FUSE2", "0")
+    with _lat(shape, C=C) as L:
+        L.upload(phi0)
+        L.step(9)
+        ref = L.download()
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    monkeypatch.setenv("SQ_FUSE2_Z", str(zb))
+    with _lat(shape, C=C) as L:
+        assert "tb2" in L.kernel_name, L.kernel_name
+        L.upload(phi0)
+        for n in (1, 4, 3, 1):
+            L.step(n)
+        got = L.download()
+        assert L.step_counter == 9
+    assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+    if C == 0.0:
+        assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 9, C=0.0))
+
+
+def test_fused_two_step_full_size_256(gpu, oracle_mod, monkeypatch):
+    """C2 at full size: 40 steps as 20 fused launches == 40 single steps."""
+    shape = (256, 256, 256)
+    phi0 = _init(oracle_mod, shape, amp=0.5)
+    outs = []
+    for fz in ("0", "1"):
+        monkeypatch.setenv("SQ_FUSE2", fz)
+        with _lat(shape, dtau=0.01, m2=1.0, lam=1.0) as L:
+            assert ("tb2" in L.kernel_name) == (fz == "1")
+            L.upload(phi0)
+            L.step(40)
+            outs.append(L.download())
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_fused_two_step_guard_and_rollback(gpu, oracle_mod, monkeypatch):
+    """A clamp / NaN in either fused step raises the frame's guard flag."""
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    shape = (256, 8, 8)
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    phi0[3, 4, 5] = np.float32(5e3)
+    phi0[6, 1, 130] = np.float32("nan")
+    with _lat(shape, C=0.0, loops=4) as L:
+        assert "tb2" in L.kernel_name
+        L.upload(phi0)
+        L.step(2)
+        assert np.array_equal(L.download(), _oracle_run(oracle_mod, shape, phi0, 2, C=0.0))
+    with _lat(shape, loops=4) as L:
+        L.upload(phi0)
+        assert not L.run_frame()
+        back = L.download()
+        assert np.array_equal(back[~np.isnan(phi0)], phi0[~np.isnan(phi0)])
+    phi1 = _init(oracle_mod, shape, amp=0.3)
+    with _lat(shape, loops=4) as L:
+        L.upload(phi1)
+        assert L.run_frame()
 
 
 @pytest.mark.parametrize("shape", [(512, 4, 6), (1024, 2, 5), (512, 8, 9)])
