@@ -135,7 +135,9 @@ struct sq_ctx {
     // persistent multi-step launches (single periodic slab; SQ_PERSIST=1: on)
     int pblocks = 0;                // co-resident blocks of the persistent kernel (0: per-step launches)
     int pU = 1;                     // units per wave per step (pblocks * 4 * pU = units)
-    int tbz = 0;                    // two-step fused launches: output planes per block (0: off)
+    int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
+    bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
+    int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
     int pchunk = 500;               // max steps per persistent launch (SQ_PERSIST_STEPS)
     unsigned int *pdone = nullptr;  // per-unit completion stamps
     size_t pdone_bytes = 0;
@@ -311,27 +313,43 @@ int phi4_persist_steps(sq_ctx *c, int n) {
     return SQ_OK;
 }
 
-// Single slab covering the lattice: steps s and s+1 in one launch
-// (sq_phi4.hip, phi4_tb2_kernel); the output lands in the other buffer.
-int phi4_tb2_pair(sq_ctx *c) {
-    Slab &s = c->slabs[0];
-    sq::Phi4StepArgs a = phi4_base_args(c, s, c->cur);
-    a.zlo = 0;
-    a.zhi = s.nz;
-    a.zstep = c->tbz;
-    a.zc = c->tbz;
-    a.nzc = (s.nz + c->tbz - 1) / c->tbz;
-    a.periodic = 1;
+// Steps s and s+1 on planes [zlo, zhi) of slab s in one launch
+// (sq_phi4.hip, phi4_tb2_kernel): reads buffer in_buf, writes in_buf ^ 1.
+int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo, int zhi, int periodic,
+                   bool timed) {
+    if (zhi <= zlo) return SQ_OK;
+    sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
+    // planes per block: pinned, or as many as make one round of tb_blocks
+    // blocks (a ragged second round costs more than the deeper chunks)
+    const int nyg = c->Ly / 8, span = zhi - zlo;
+    // (the slabs of a loopback decomposition run concurrently on their own streams)
+    const int nzc_t = std::max(1, c->tb_blocks / (nyg * (int)c->slabs.size()));
+    const int zb = c->tbz_pin ? c->tbz : std::max(1, (span + nzc_t - 1) / nzc_t);
+    a.zlo = zlo;
+    a.zhi = zhi;
+    a.zstep = zb;
+    a.zc = zb;
+    a.nzc = (span + zb - 1) / zb;
+    a.periodic = periodic;
     a.nxseg = 1;
-    a.nyg = c->Ly / 8;
+    a.nyg = nyg;
     a.nunits = a.nyg * a.nzc;
     EvPair *e = nullptr;
-    if (c->profiling == 1) {
+    if (timed && c->profiling == 1) {
         int rc = ev_take(c, &e);
         if (rc) return rc;
         c->ev_extra_steps += 1;
     }
-    SQ_HIP(sq::phi4_tb2_launch(a, s.sA, e ? e->a : nullptr, e ? e->b : nullptr));
+    SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    return SQ_OK;
+}
+
+// Single slab covering the lattice: steps s and s+1 in one launch; the
+// output lands in the other buffer.
+int phi4_tb2_pair(sq_ctx *c) {
+    Slab &s = c->slabs[0];
+    int rc = phi4_tb2_range(c, s, c->cur, s.sA, 0, s.nz, 1, true);
+    if (rc) return rc;
     c->cur ^= 1;
     count_step(c);
     count_step(c);
@@ -427,10 +445,27 @@ int phi4_block(sq_ctx *c, int g) {
         if (rc) return rc;
     }
     count_step(c);
-    // 4. steps 1..g-1 on the shrinking extended range; the last one edges first
+    // 4. steps 1..g-1 on the shrinking extended range; the last one edges
+    //    first.  With the two-step kernel (tbz > 0) the steps before the last
+    //    go in pairs: the pair (st, st+1) writes step st+1's range and reads
+    //    step st-1's, both inside the ghost zone; ib tracks the buffer that
+    //    holds the latest step (a pair flips it once, not twice).
     std::vector<char> edges_recorded(c->slabs.size(), 0);  // per slab: slabs of a decomposition differ in nz
-    for (int st = 1; st < g; ++st) {
-        const int in_buf = cur ^ (st & 1);
+    int ib = cur ^ 1;
+    for (int st = 1; st < g;) {
+        if (c->tbz > 0 && st + 1 < g - 1) {
+            const int e = g - 2 - st;  // ghost planes step st+1 still updates on either side
+            for (auto &s : c->slabs) {
+                int rc = phi4_tb2_range(c, s, ib, s.sA, -e, s.nz + e, 0, true);
+                if (rc) return rc;
+            }
+            ib ^= 1;
+            count_step(c);
+            count_step(c);
+            st += 2;
+            continue;
+        }
+        const int in_buf = ib;
         const bool split = st == g - 1;
         for (size_t i = 0; i < c->slabs.size(); ++i) {
             Slab &s = c->slabs[i];
@@ -448,14 +483,16 @@ int phi4_block(sq_ctx *c, int g) {
             }
             if (rc) return rc;
         }
+        ib ^= 1;
         count_step(c);
+        ++st;
     }
     for (size_t i = 0; i < c->slabs.size(); ++i) {
         Slab &s = c->slabs[i];
         SQ_HIP(hipEventRecord(s.evA, s.sA));
         if (!edges_recorded[i]) SQ_HIP(hipEventRecord(s.evE, s.sA));
     }
-    c->cur = cur ^ (g & 1);
+    c->cur = ib;
     return SQ_OK;
 }
 
@@ -681,14 +718,28 @@ int create_phi4(sq_ctx *c) {
     // Opt-in (SQ_PERSIST=1): bit-identical, but measured 55 us per 256^3 step
     // (31 us with the dependency waits removed) vs 21.5 us for per-step
     // launches (profiles/r01/persist_ab.log).
-    // Two steps per launch on 256-wide single-slab lattices (SQ_FUSE2=0: off;
-    // SQ_FUSE2_Z: output planes per block).  256^3: 19.5 vs 22.0 us per step
-    // on the same box; z = 16 (512 blocks, two per CU) measured best of
-    // 8/11/12/16/22/32 (profiles/r01/fuse2_sweep.log).
+    // Two steps per launch on 256-wide lattices (SQ_FUSE2=0: off; SQ_FUSE2_Z:
+    // pin the output planes per block), single slab and deep-halo slabs alike.
+    // 256^3: 19.5 vs 22.0 us per step on the same box; one round of two
+    // blocks per CU (z = 16 at 256^3) measured best of z = 8/11/12/16/22/32
+    // (profiles/r01/fuse2_sweep.log), so every launch picks the depth that
+    // makes one such round.
+    // Loopback decompositions (several slabs on one GPU, a rehearsal mode)
+    // keep one step per launch unless SQ_FUSE2=1: there the concurrent slab
+    // launches ran slower fused (29.1 vs 25.4 us per step, 2 slabs of 128
+    // planes), while one RCCL slab of 256 planes gains (24.2 vs 26.0,
+    // profiles/r01/fuse2_slabs.log).
     const char *fe = getenv("SQ_FUSE2");
-    if (!(fe && atoi(fe) == 0) && p.comm == SQ_COMM_NONE && sq::phi4_tb2_supported(c->Lx, c->Ly, c->slabs[0].nz)) {
+    const bool fuse = fe ? atoi(fe) != 0 : p.comm != SQ_COMM_LOOPBACK;
+    if (fuse && sq::phi4_tb2_supported(c->Lx, c->Ly) && (p.comm != SQ_COMM_NONE || c->slabs[0].nz >= 2)) {
         c->tbz = 16;
-        if (const char *z = getenv("SQ_FUSE2_Z")) c->tbz = std::max(1, atoi(z));
+        if (const char *z = getenv("SQ_FUSE2_Z")) {
+            c->tbz = std::max(1, atoi(z));
+            c->tbz_pin = true;
+        }
+        int ncu = 0;
+        SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
+        c->tb_blocks = 2 * std::max(1, ncu);  // 68 VGPRs, 10 waves: two blocks per CU
     }
     const char *pe = getenv("SQ_PERSIST");
     if (p.comm == SQ_COMM_NONE && pe && atoi(pe) != 0) {
@@ -1252,8 +1303,11 @@ int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
     if (pf == 2 && !(c->geom.qx == 64 && c->geom.v == 1)) pf = 1;
     if (pf >= 3 && c->geom.qx != 64) pf = 1;
     if (pf == 5 && ms) pf = 3;
-    if (c->tbz > 0)
+    if (c->tbz > 0 && c->tbz_pin)
         snprintf(name, cap, "phi4_tb2_kernel<%s> (2 steps per launch) z=%d", nz ? "true" : "false", c->tbz);
+    else if (c->tbz > 0)
+        snprintf(name, cap, "phi4_tb2_kernel<%s> (2 steps per launch) one round of %d blocks", nz ? "true" : "false",
+                 c->tb_blocks);
     else if (c->pblocks > 0)
         snprintf(name, cap,
                  "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks, %d units per wave",

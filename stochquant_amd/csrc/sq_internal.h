@@ -60,10 +60,11 @@ struct Phi4PersistArgs {
 int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu);
 hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s);
 
-// Two steps per launch (steps s and s+1, s = a.s_hi:a.s_lo) on a single
-// periodic slab: a.zc = output planes per block, a.nyg = Ly / 8 y-bands,
-// a.nzc z-chunks, a.nunits = blocks; bit-identical to two step launches.
-bool phi4_tb2_supported(int Lx, int Ly, int nz);
+// Two steps per launch (steps s and s+1, s = a.s_hi:a.s_lo) on planes
+// [a.zlo, a.zhi) (a single periodic slab: [0, nz)): a.zc = output planes per
+// block, a.nyg = Ly / 8 y-bands, a.nzc z-chunks, a.nunits = blocks; the
+// input must be valid on [zlo-2, zhi+2).  Bit-identical to two step launches.
+bool phi4_tb2_supported(int Lx, int Ly);
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t start = nullptr,
                            hipEvent_t stop = nullptr);
 

@@ -534,7 +534,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 
 // ----------------------------------------------------- two-step fusion ----
 // Steps s and s+1 in one pass over the field (temporal blocking), for
-// 256-wide rows on a single periodic slab.  A block of kTbWaves = 10 waves
+// 256-wide rows: a single periodic slab, or the planes [zlo, zhi) of a slab
+// whose input is valid on [zlo-2, zhi+2) (deep-halo blocks).  A block of kTbWaves = 10 waves
 // owns kTbRows = 8 output rows [y0, y0+8) of a z-chunk [z0, z1); wave w
 // holds row y0-1+w.  Marching p over [z0-1, z1]:
 //   1. every wave loads input plane p+1 (its row and both y-halo rows) and
@@ -552,8 +553,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 constexpr int kTbRows = 8;
 constexpr int kTbWaves = kTbRows + 2;
 
-__device__ __forceinline__ int tb_pidx(const Phi4StepArgs &A, int zl) {  // periodic, |overflow| <= 2
-    return (zl < 0 ? zl + A.nz : (zl >= A.nz ? zl - A.nz : zl)) + A.gz;
+// Padded plane of local plane zl: the periodic slab wraps (|overflow| <= 2),
+// a slab of a decomposition reads its ghost zone.
+__device__ __forceinline__ int tb_pidx(const Phi4StepArgs &A, int zl) {
+    if (A.periodic) zl = zl < 0 ? zl + A.nz : (zl >= A.nz ? zl - A.nz : zl);
+    return zl + A.gz;
 }
 
 template <bool NZ>
@@ -601,11 +605,11 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, int p, int z0, c
         const float m = fmaxf(fmaxf(fabsf(T2.x), fabsf(T2.y)), fmaxf(fabsf(T2.z), fabsf(T2.w)));
         bad |= (int)(m >= A.clampv);
     }
-    const int sl = p % 3;
+    const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
     lds[sl][w][lane] = T2;
     __syncthreads();
     if (doB) {
-        const int sp = (p + 2) % 3;  // slot of plane p-1
+        const int sp = ((p + 2) % 3 + 3) % 3;  // slot of plane p-1
         const float4 up = lds[sp][w - 1][lane], dn = lds[sp][w + 1][lane];
         const float4 o = site_update4<NZ>(T1, from_left_lane(T1.w), from_right_lane(T1.x), up, dn, T0, T2, xb, A);
         if (A.flag != nullptr) {
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(kTbWaves * 64) void phi4_tb2_kernel(const Phi4StepA
     const uint32_t vm = (uint32_t)((ym * Lx + 4 * lane) * 4), vp = (uint32_t)((yp * Lx + 4 * lane) * 4);
     const uint32_t qoff = (uint32_t)((y * Lx + 4 * lane) >> 2);
     const bool outw = w >= 1 && w <= kTbRows;
-    const int z0 = zk * A.zc, z1 = min(z0 + A.zc, A.nz);
+    const int z0 = A.zlo + zk * A.zc, z1 = min(z0 + A.zc, A.zhi);
     const size_t plane = (size_t)Lx * (size_t)Ly;
     const uint32_t pbytes = (uint32_t)(plane * sizeof(float));
     const uint32_t qplane = (uint32_t)(plane >> 2);
@@ -882,10 +886,13 @@ static const void *persist_fn(const Phi4Geom &g, bool ms, bool nz) {
     return nullptr;
 }
 
-bool phi4_tb2_supported(int Lx, int Ly, int nz) { return Lx == 256 && Ly % kTbRows == 0 && nz >= 2; }
+bool phi4_tb2_supported(int Lx, int Ly) { return Lx == 256 && Ly % kTbRows == 0; }
 
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (!phi4_tb2_supported(a.Lx, a.Ly, a.nz) || !a.periodic || a.nunits <= 0) return hipErrorInvalidValue;
+    if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0) return hipErrorInvalidValue;
+    if (a.periodic ? (a.nz < 2 || a.zlo != 0 || a.zhi != a.nz)
+                   : (a.zlo - 2 < -a.gz || a.zhi + 2 > a.nz + a.gz))  // input planes outside the buffer
+        return hipErrorInvalidValue;
     const dim3 grid((unsigned)a.nunits), block(kTbWaves * 64);
     const void *fn = a.sig != 0.0f ? (const void *)&phi4_tb2_kernel<true> : (const void *)&phi4_tb2_kernel<false>;
     Phi4StepArgs q = a;

@@ -371,6 +371,50 @@ def test_fused_two_step_bitwise(gpu, oracle_mod, monkeypatch, shape, zb, C):
         assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 9, C=0.0))
 
 
+@pytest.mark.parametrize("shape,ghost,nslabs,steps", [((256, 8, 24), 2, 2, 7), ((256, 8, 24), 4, 3, 13),
+                                                      ((256, 16, 40), 5, 3, 11), ((256, 16, 40), 8, 2, 17),
+                                                      ((256, 8, 30), 3, 4, 9)])
+def test_fused_two_step_deep_halo_bitwise(gpu, oracle_mod, monkeypatch, shape, ghost, nslabs, steps):
+    """Deep-halo blocks with the inner steps fused in pairs (the pair writes the
+    second step's shrinking ghost range) == the single-slab run with one step
+    per launch, bit for bit, over several blocks and a partial one."""
+    phi0 = _init(oracle_mod, shape)
+    monkeypatch.setenv("SQ_FUSE2", "0")
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(steps)
+        mono = L.download()
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    monkeypatch.setenv("SQ_FUSE2_Z", "3")
+    monkeypatch.setenv("SQ_GHOST", str(ghost))
+    with _lat(shape, comm="loopback", nslabs=nslabs) as L:
+        assert "tb2" in L.kernel_name
+        L.upload(phi0)
+        for n in (1, steps - 1):
+            L.step(n)
+        assert np.array_equal(mono, L.download())
+
+
+def test_fused_two_step_rccl_frames(gpu, oracle_mod, monkeypatch):
+    """RCCL self-exchange slab with fused inner steps, run as frames."""
+    from stochquant_amd import unique_id
+    shape = (256, 16, 32)
+    phi0 = _init(oracle_mod, shape)
+    monkeypatch.setenv("SQ_FUSE2", "0")
+    with _lat(shape, loops=7) as L:
+        L.upload(phi0)
+        for _ in range(3):
+            assert L.run_frame()
+        mono = L.download()
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    monkeypatch.setenv("SQ_GHOST", "6")
+    with _lat(shape, loops=7, comm="rccl", nranks=1, rank=0, comm_id=unique_id()) as L:
+        L.upload(phi0)
+        for _ in range(3):
+            assert L.run_frame()
+        assert np.array_equal(mono, L.download())
+
+
 def test_fused_two_step_full_size_256(gpu, oracle_mod, monkeypatch):
     """C2 at full size: 40 steps as 20 fused launches == 40 single steps."""
     shape = (256, 256, 256)
