@@ -3,26 +3,32 @@
 Workload (BASELINE.json configs[1]): a 256^3 fp32 lattice
 PER GPU, periodic, Δτ = 0.01, m² = 1, λ = 1, φ₀ = 0.1·normal; one "step" = one
 Langevin update of every site (sq_step).  N = 1: one GPU, one HIP stream, z
-wraps in-kernel.  N > 1 (launched by torch.distributed.run, one process per
-GPU): weak scaling, global lattice 256 x 256 x (256 N) cut into z-slabs, halo
-planes exchanged over RCCL (xGMI) on a second stream, overlapped with the
-interior planes.
+wraps in-kernel.  N > 1: one process per GPU, weak scaling, global lattice
+256 x 256 x (256 N) cut into z-slabs, deep ghost zones exchanged over RCCL
+(xGMI) on a second stream, overlapped with the interior planes.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--size L]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size L] [--strong]
 
-Prints ONE JSON line (rank 0).  `value` = all site updates of all ranks / max
-over ranks of the barrier-bracketed wall time of the K timed steps.
-`roofline.achieved` = 8 algorithmic bytes per site update x the
-site updates of one launch / mean duration of the launches in the timed
-region (hipEvents recorded on the kernel's own stream by libstochquant.so).
-At N = 1 on 256-wide lattices a launch fuses two steps (phi4_tb2_kernel), so
-it moves the field once per two updates: `hbm_min_GBps` is the rate of that
-one read + one write, `traffic` the PMC-measured bytes per launch.  `cpu_baseline` = the oracle's C port
-of the same step (OpenMP over the box's host cores) on a bounded sample.
+With --gpus N > 1 and no torch.distributed launcher around it, the process
+spawns the N rank processes itself (fresh interpreters, RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_* set, before anything touches a GPU) and relays rank 0's
+line.
+
+Timing: first a clock-settle phase (--settle-ms of steps, untimed, reported as
+`settle_ms` / `settle_steps`: the short driver invocation --warmup 5 would
+otherwise time ramping clocks), then W warm-up steps, then EXACTLY K timed steps
+bracketed by barrier + device synchronisation; `value` = all site updates of
+all ranks / max over ranks of that wall time.  `roofline.achieved` = 8
+algorithmic bytes per site update x the updates of one launch
+/ the mean launch duration from one hipEvent pair on the kernel's own stream
+around the K timed steps (`frac_kernel`); `frac_wall` is the same bytes over
+the wall time behind `value`.  Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,8 +44,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
-    ap.add_argument("--warmup", type=int, default=2000,
-                    help="untimed steps first (clocks settle: 2000 vs 200 measured +2.8 %%, profiles/r01/warmup_ab.log)")
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--settle-ms", type=float, default=1500.0,
+                    help="untimed steps for at least this long before the warm-up (clock settle)")
     ap.add_argument("--size", type=int, default=256, help="per-GPU lattice edge (default 256 = config C2)")
     ap.add_argument("--dtau", type=float, default=0.01)
     ap.add_argument("--comm", choices=["auto", "rccl", "loopback"], default="auto",
@@ -56,13 +63,67 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """Start n rank processes of this script (no GPU call has been made here),
+    relay rank 0's stdout, return the worst exit code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].stdout.read().decode()
+    rcs = []
+    for p in procs:
+        rcs.append(p.wait())
+    if any(rcs):  # a failed rank: make sure none is left behind
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return max(rcs, key=abs)
+
+
+def cpu_share():
+    """Host CPUs this job may use: the affinity mask, bounded by a cgroup quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(L, dtau, target_s):
-    """Oracle (C port of the same step, OpenMP) on a bounded sample of the workload."""
-    import numpy as np
+    """Oracle (C port of the same step, OpenMP over the job's CPU share) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test/baseline infrastructure only: timed as the CPU baseline, never as the product
     oracle.build()
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores = cpu_share()
     shape = (L, L, L)
     p = oracle.phi4_params(shape, dtau, 1.0, 1.0, 0x5EED)
     phi = oracle.phi4_init(p, 0.1)
@@ -75,33 +136,34 @@ def cpu_baseline(L, dtau, target_s):
         phi = oracle.phi4_step(p, phi, 1 + s, cores)
     dt = time.perf_counter() - t0
     return {"value": float(L ** 3 * n / dt), "unit": "site-updates/s", "cores": cores, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"{n} steps of the {L}^3 fp32 phi^4 Langevin step (oracle/orc_phi4.c, OpenMP, "
-                      f"{cores} threads), {dt:.2f} s"}
+                      f"{cores} threads = this job's CPU share of {os.cpu_count()} host CPUs), {dt:.2f} s"}
 
 
-def pmc_traffic(L, nranks, kernel):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if it matches this workload."""
+def pmc_record(L, nranks, kernel):
+    """The committed rocprofv3 PMC summary for this workload and kernel, if any (it is
+    measured by scripts/pmc_r02.sh on this same command, not inside this run)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
-        return None
-    same_kernel = ("phi4_tb2_kernel" in d.get("kernel", "")) == ("phi4_tb2_kernel" in kernel)
-    if d.get("size") == L and d.get("nranks", 1) == nranks and same_kernel:
-        return d.get("hbm_bytes_per_launch")
-    return None
+        return None, None
+    k = kernel.split("<")[0]
+    if d.get("size") == L and d.get("nranks", 1) == nranks and k and k in d.get("kernel", ""):
+        return d, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if a.gpus != world:
-        if world == 1 and a.gpus > 1:
-            sys.exit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
-        a.gpus = world
+    a.gpus = world
     import torch
     import torch.distributed as dist
     from stochquant_amd import Phi4Lattice, unique_id, _lib
@@ -134,13 +196,27 @@ def main():
 
     if slab_path:
         lat.step(84)   # setup: the ghost-depth trial blocks (3 x (4 + 8 + 16) steps) when autotuning
+    # clock settle: untimed batches until settle_ms have passed on rank 0 (every
+    # rank runs the same batches: the slab exchanges must pair up)
+    settle_steps = 0
+    t_settle = time.perf_counter()
+    while True:
+        lat.step(50)
+        lat.sync()
+        settle_steps += 50
+        go = torch.tensor([1 if (time.perf_counter() - t_settle) * 1e3 < a.settle_ms else 0], dtype=torch.int32)
+        if world > 1:
+            dist.broadcast(go, src=0)
+        if not int(go.item()):
+            break
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
     lat.step(a.warmup)
     lat.sync()
     torch.cuda.synchronize()
     lat.perf_reset()
     # mode 2: ONE hipEvent pair on the step-kernel stream around the K timed
     # launches (per-launch dispatch events cost ~4 us of wall per step, see
-    # DESIGN.md §Measurement); avg launch = region / K, inter-kernel gaps included.
+    # DESIGN.md §6); avg launch = region / launches, inter-kernel gaps included.
     lat.set_profiling(0 if a.no_profile_events else 2)
     barrier()
     torch.cuda.synchronize()
@@ -161,19 +237,19 @@ def main():
     sites_local = lat.nz_local * L * L
     total_updates = float(shape[0] * shape[1] * shape[2]) * a.steps
     value = total_updates / t
+    nslabs = a.slabs if (world == 1 and a.comm == "loopback") else 1
+    launches = max(1, perf["kernel_launches"])
+    spl = perf["steps"] * nslabs / launches          # steps per launch, measured (2 = two-step fused)
     if perf["step_kernel_launches"] > 0:
-        # region mean per step on the (interior) step-kernel stream; with slabs it
-        # spans interior + halo + boundary, so charge all local sites to it
-        avg_ms = perf["step_kernel_ms"] / perf["step_kernel_launches"]
-        sites_per_launch = sites_local
+        # event region on the (interior) step-kernel stream: it spans every
+        # launch of the timed steps, so charge all local sites to it
+        step_ms = perf["step_kernel_ms"] / perf["step_kernel_launches"]
     else:
-        avg_ms = t * 1e3 / a.steps
-        sites_per_launch = sites_local
-    # two-step fused launches (phi4_tb2_kernel) update every site twice
+        step_ms = t * 1e3 / a.steps
+    launch_ms = step_ms * spl
+    achieved = BYTES_PER_SITE * sites_local / (step_ms * 1e-3) / 1e9
+    achieved_wall = BYTES_PER_SITE * value / 1e9
     kname = lat.kernel_name
-    spl = 2 if "2 steps per launch" in kname else 1
-    launch_ms = avg_ms * spl
-    achieved = BYTES_PER_SITE * sites_per_launch * spl / (launch_ms * 1e-3) / 1e9
     out = None
     if rank == 0:
         copy = None
@@ -184,6 +260,8 @@ def main():
                 copy = round(g.value, 1)
         except Exception:
             copy = None
+        rec, rec_path = pmc_record(L, world, kname) if not slab_path else (None, None)
+        fused = "tb2" in kname and not slab_path
         out = {
             "metric": METRIC,
             "value": value,
@@ -191,6 +269,8 @@ def main():
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "settle_ms": round(settle_ms, 1),
+            "settle_steps": settle_steps,
             "ms_per_step": t * 1e3 / a.steps,
             "higher_is_better": True,
             "scaling": "strong" if a.strong else "weak",
@@ -206,28 +286,37 @@ def main():
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
                 "ghost_depth": lat.ghost[0] if slab_path else None,
                 "parallelism": "single GPU, one stream" if not slab_path else
-                               f"z-slab x{world} ({a.comm if world == 1 else 'rccl'}), halo + boundary planes on "
+                               f"z-slab x{world} ({a.comm if world == 1 else 'rccl'}), halo exchange on "
                                f"stream B, interior on stream A",
             },
             "roofline": {
-                "bound": "hbm",
+                # the fused kernel moves the field once per two updates and is issue-bound
+                # (PMC: profiles/r02/); the per-step kernel at 512^3+ is HBM-bound
+                "bound": "valu" if fused else "hbm",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic": pmc_traffic(L, world, kname),
+                "frac_kernel": round(achieved / HBM_PEAK_GBPS, 4),
+                "frac_wall": round(achieved_wall / HBM_PEAK_GBPS, 4),
+                "achieved_wall": round(achieved_wall, 1),
+                "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time",
+                "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+                "traffic_source": (f"cached: {rec_path}, rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this "
+                                   f"bench command (not measured inside this run)") if rec else None,
+                "valu_issue_frac": rec.get("valu_issue_frac") if rec else None,
                 "kernel": kname,
                 "timing": "hipEvent pair on the kernel stream around the timed launches (region mean)"
                           if perf["step_kernel_launches"] > 0 else "wall clock",
-                "steps_per_launch": spl,
-                "algorithmic_bytes_per_launch": BYTES_PER_SITE * sites_per_launch * spl,
+                "steps_per_launch": round(spl, 3),
+                "kernel_launches_timed": perf["kernel_launches"],
+                "algorithmic_bytes_per_launch": round(BYTES_PER_SITE * sites_local * spl),
                 "avg_launch_us": round(launch_ms * 1e3, 3),
-                "avg_step_us": round(avg_ms * 1e3, 3),
-                "launches_timed": perf["step_kernel_launches"] // spl,
+                "avg_step_us": round(step_ms * 1e3, 3),
                 # the least HBM traffic a launch can have (one read + one write
                 # of the field) and the rate it moved at
-                "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_per_launch,
-                "hbm_min_GBps": round(BYTES_PER_SITE * sites_per_launch / (launch_ms * 1e-3) / 1e9, 1),
+                "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_local,
+                "hbm_min_GBps": round(BYTES_PER_SITE * sites_local / (launch_ms * 1e-3) / 1e9, 1),
             },
             "hbm_copy_peak_GBps": copy,
             "field_check": {"rms": (m["sum2"] / sites_local) ** 0.5, "maxabs": m["maxabs"]},

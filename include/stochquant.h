@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SQ_ABI_VERSION 1
+#define SQ_ABI_VERSION 2
 
 /* status codes */
 #define SQ_OK 0
@@ -69,12 +69,31 @@ typedef struct sq_params {
 
 typedef struct sq_perf_t {
     long long steps;            /* Langevin steps executed since the last sq_perf_reset */
-    long long site_updates;     /* local sites x steps */
+    long long site_updates;     /* local sites x steps (ghost-zone recomputation not counted) */
     double step_kernel_ms;      /* sum of hipEvent-timed durations of the step kernels (profiling on) */
-    long long step_kernel_launches;
+    long long step_kernel_launches; /* steps covered by step_kernel_ms (profiling on) */
     double frame_ms;            /* wall time inside sq_run_frame / sq_step (host clock) */
     double halo_bytes;          /* bytes sent by halo exchange */
+    long long kernel_launches;  /* step-kernel launches issued (any profiling mode): steps / this =
+                                   steps per launch (2 for two-step fused launches; a slab block of
+                                   G steps issues its core, rim, pairs and edge launches) */
+    long long fused_steps;      /* steps executed inside two-step fused launches */
 } sq_perf_t;
+
+/* One operation of a deep-halo block (PHI4 slab decompositions),
+ * in issue order; see sq_phi4_block_plan. */
+#define SQ_OP_EXCHANGE 0       /* stream B: after the previous block's SQ_OP_EDGES_DONE, send the ghost-depth
+                                  edge planes of the latest field to both z-neighbours, receive their ghosts */
+#define SQ_OP_STEP 1           /* stream A: step `step` on planes [lo, hi) (and [lo2, hi2) when lo2 < hi2) */
+#define SQ_OP_PAIR 2           /* stream A: steps `step`, `step`+1 in one launch; output [lo, hi), reads
+                                  [lo-2, hi+2) of the latest field */
+#define SQ_OP_WAIT_EXCHANGE 3  /* stream A waits for this block's exchange */
+#define SQ_OP_EDGES_DONE 4     /* stream A: the planes the next exchange sends are final (event) */
+typedef struct sq_block_op {
+    int kind;                  /* SQ_OP_* */
+    int step;                  /* block-relative index of the (first) step computed */
+    int lo, hi, lo2, hi2;      /* local plane ranges; negative = lower ghost zone, >= nz = upper */
+} sq_block_op;
 
 typedef struct sq_ctx sq_ctx;
 
@@ -144,6 +163,17 @@ int sq_phi4_kernel(sq_ctx *ctx, char *name, size_t cap);
  * first sq_step / sq_run_frame calls) and the depth allocated; 0, 0 for a
  * single periodic slab. */
 int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
+/* The launch schedule of one deep-halo block (pure host logic, no device
+ * needed; the product's phi4_block executes exactly this list): a slab of nz
+ * planes with a ghost zone of `ghost` planes (the exchange depth G) running
+ * g <= G steps; fuse2 != 0 runs the inner steps as two-step pairs, edge_first
+ * != 0 computes the last step's edge planes first.  Writes *nops ops (at most
+ * cap).  sq_phi4_pick_ghost returns the index of the fastest candidate of the
+ * rank-max-reduced per-step times ms[n] (the ghost-depth trial, identical on
+ * every rank once the times are reduced). */
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
+                       int *nops);
+int sq_phi4_pick_ghost(const double *ms, int n);
 /* PHI4 observables over this process' slab: out[0] = sum phi, out[1] = sum
  * phi^2, out[2] = max |phi| (double accumulation on device). */
 int sq_moments(sq_ctx *ctx, double out[3]);

@@ -81,6 +81,8 @@ def lib():
         L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_uint64]
         L.orc_phi4_init.argtypes = [ctypes.POINTER(Phi4), ctypes.c_float, _F]
+        L.orc_phi4_step_range.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         L.orc_phi4_sigma.restype = ctypes.c_float
         L.orc_phi4_sigma.argtypes = [ctypes.c_float, ctypes.c_double]
         _lib = L
@@ -201,6 +203,17 @@ def phi4_step_slab(p, padded, z0, step):
     out = np.empty((nz,) + a.shape[1:], dtype=np.float32)
     lib().orc_phi4_step_slab(ctypes.byref(p), a.ctypes.data_as(_F), out.ctypes.data_as(_F), nz, z0, step)
     return out
+
+
+def phi4_step_range(p, src, dst, gpad, lo, hi, z0, step):
+    """Update planes [lo, hi) (local, may reach into the ghost zones) of the
+    padded slab `dst` ((nz + 2 gpad, Ly, Lx) float32, modified in place) from
+    the padded slab `src`; global z wraps modulo Lz."""
+    assert src.dtype == np.float32 and dst.dtype == np.float32 and src.flags.c_contiguous and dst.flags.c_contiguous
+    nz = src.shape[0] - 2 * gpad
+    assert -gpad < lo and hi < nz + gpad, "the range needs one readable plane on either side"
+    lib().orc_phi4_step_range(ctypes.byref(p), src.ctypes.data_as(_F), dst.ctypes.data_as(_F), nz, gpad, lo, hi,
+                              z0, step)
 
 
 def phi4_init(p, amp):

@@ -93,6 +93,20 @@ void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, 
                    out + (size_t)z * plane, z0 + (uint64_t)z, step);
 }
 
+void orc_phi4_step_range(const orc_phi4 *p, const float *in, float *out, int nz, int gpad, int lo, int hi,
+                         uint64_t z0, uint64_t step)
+{
+    const size_t plane = (size_t)p->Lx * p->Ly;
+    const int64_t Lz = p->Lz;
+    (void)nz;
+    for (int zl = lo; zl < hi; ++zl) {
+        const int64_t zg = (((int64_t)z0 + zl) % Lz + Lz) % Lz;
+        const size_t c = (size_t)(zl + gpad);
+        phi4_plane(p, in + c * plane, in + (c - 1) * plane, in + (c + 1) * plane, out + c * plane,
+                   (uint64_t)zg, step);
+    }
+}
+
 void orc_phi4_init(const orc_phi4 *p, float amp, float *out)
 {
     const size_t n = (size_t)p->Lx * p->Ly * p->Lz;

@@ -105,6 +105,13 @@ typedef struct {
 void orc_phi4_step(const orc_phi4 *p, const float *in, float *out, uint64_t step, int nthreads);
 /* Slab with explicit ghost planes: in = nz+2 planes, out = nz planes. */
 void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, uint64_t z0, uint64_t step);
+/* Deep-halo form (the slab path's shrinking ranges): `in` and `out` are padded
+ * slabs of nz + 2*gpad planes (local plane zl at padded index zl + gpad); the
+ * planes [lo, hi) of `out` are updated from `in` (which must be valid on
+ * [lo-1, hi+1)), every other plane of `out` is left alone.  Global z of local
+ * plane zl = (z0 + zl) mod Lz (ghost-zone planes wrap). */
+void orc_phi4_step_range(const orc_phi4 *p, const float *in, float *out, int nz, int gpad, int lo, int hi,
+                         uint64_t z0, uint64_t step);
 /* Derived float parameters exactly as the product computes them. */
 float orc_phi4_sigma(float h, double C);
 float orc_phi4_lam6(float lam);

@@ -65,7 +65,18 @@ class SqPerf(ctypes.Structure):
         ("step_kernel_launches", ctypes.c_longlong),
         ("frame_ms", ctypes.c_double),
         ("halo_bytes", ctypes.c_double),
+        ("kernel_launches", ctypes.c_longlong),
+        ("fused_steps", ctypes.c_longlong),
     ]
+
+
+class SqBlockOp(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("step", ctypes.c_int), ("lo", ctypes.c_int), ("hi", ctypes.c_int),
+                ("lo2", ctypes.c_int), ("hi2", ctypes.c_int)]
+
+
+SQ_OP_EXCHANGE, SQ_OP_STEP, SQ_OP_PAIR, SQ_OP_WAIT_EXCHANGE, SQ_OP_EDGES_DONE = range(5)
+ABI_VERSION = 2
 
 
 _P = ctypes.c_void_p
@@ -97,6 +108,9 @@ SIGNATURES = {
     "sq_load_field": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_int]),
     "sq_phi4_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "sq_phi4_ghost": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "sq_phi4_block_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
+    "sq_phi4_pick_ghost": (ctypes.c_int, [_D, ctypes.c_int]),
     "sq_qm1d_set_ordering": (ctypes.c_int, [_P, ctypes.c_int]),
     "sq_qm1d_set_lcg_seed": (ctypes.c_int, [_P, ctypes.c_ulonglong]),
     "sq_qm1d_get_lcg_seed": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),
@@ -144,7 +158,7 @@ def load(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.sq_abi_version() != 1:
+    if lib.sq_abi_version() != ABI_VERSION:
         raise StochQuantUnavailable("ABI version mismatch")
     if path is None:
         _lib = lib

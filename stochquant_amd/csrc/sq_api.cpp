@@ -132,18 +132,9 @@ struct sq_ctx {
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;
-    // persistent multi-step launches (single periodic slab; SQ_PERSIST=1: on)
-    int pblocks = 0;                // co-resident blocks of the persistent kernel (0: per-step launches)
-    int pU = 1;                     // units per wave per step (pblocks * 4 * pU = units)
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
-    int pchunk = 500;               // max steps per persistent launch (SQ_PERSIST_STEPS)
-    unsigned int *pdone = nullptr;  // per-unit completion stamps
-    size_t pdone_bytes = 0;
-    int *perr = nullptr;            // a dependency wait timed out
-    unsigned int pstamp = 0;        // stamp of the last completed step
-    bool ppending = false;          // a persistent launch since the last error check
     long long ev_extra_steps = 0;   // profiling mode 1: steps beyond the first in timed launches
     ncclComm_t comm = nullptr;
     // profiling: 0 off, 1 per launch (hipExtLaunchKernel dispatch timestamps),
@@ -251,6 +242,7 @@ int phi4_launch_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int 
         if (rc) return rc;
     }
     SQ_HIP(sq::phi4_step_launch(a, c->geom, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    c->perf.kernel_launches += 1;
     return SQ_OK;
 }
 
@@ -264,53 +256,6 @@ void count_step(sq_ctx *c) {
     c->step += 1;
     c->perf.steps += 1;
     for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane_floats(c);
-}
-
-// Single slab covering the lattice, all n steps in persistent launches of
-// <= pchunk equal steps (sq_phi4.hip, phi4_persist_kernel).
-int phi4_persist_steps(sq_ctx *c, int n) {
-    Slab &s = c->slabs[0];
-    const int nzc = (s.nz + c->zc - 1) / c->zc;
-    const int nl = (n + c->pchunk - 1) / c->pchunk;
-    for (int l = 0; l < nl; ++l) {
-        const int m = n / nl + (l < n % nl ? 1 : 0);
-        if (c->pstamp > (1u << 30)) {  // stamps wrap-compare; restart them long before 2^31
-            SQ_HIP(hipMemsetAsync(c->pdone, 0, c->pdone_bytes, s.sA));
-            c->pstamp = 0;
-        }
-        sq::Phi4PersistArgs P{};
-        P.a[0] = phi4_base_args(c, s, c->cur);
-        P.a[0].zlo = 0;
-        P.a[0].zhi = s.nz;
-        P.a[0].zstep = c->zc;
-        P.a[0].zc = c->zc;
-        P.a[0].nzc = nzc;
-        P.a[0].periodic = 1;
-        sq::phi4_fill_units(P.a[0], c->geom);
-        P.a[1] = P.a[0];
-        P.a[1].in = P.a[0].out;
-        P.a[1].out = const_cast<float *>(P.a[0].in);
-        P.done = c->pdone;
-        P.err = c->perr;
-        P.base = c->pstamp;
-        P.nsteps = m;
-        P.U = c->pU;
-        P.nzq = nzc / c->pU;
-        EvPair *e = nullptr;
-        if (c->profiling == 1) {
-            int rc = ev_take(c, &e);
-            if (rc) return rc;
-            SQ_HIP(hipEventRecord(e->a, s.sA));
-            c->ev_extra_steps += m - 1;
-        }
-        SQ_HIP(sq::phi4_persist_launch(P, c->geom, c->pblocks, s.sA));
-        if (e) SQ_HIP(hipEventRecord(e->b, s.sA));
-        c->pstamp += (unsigned)m;
-        c->ppending = true;
-        c->cur ^= m & 1;
-        for (int i = 0; i < m; ++i) count_step(c);
-    }
-    return SQ_OK;
 }
 
 // Steps s and s+1 on planes [zlo, zhi) of slab s in one launch
@@ -341,6 +286,8 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo
         c->ev_extra_steps += 1;
     }
     SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    c->perf.kernel_launches += 1;
+    c->perf.fused_steps += 2;
     return SQ_OK;
 }
 
@@ -367,24 +314,64 @@ int phi4_periodic_step(sq_ctx *c) {
     return SQ_OK;
 }
 
-// Deep-halo block of g <= gz steps on every slab.
-//   stream B: after the previous block (evA), exchange gz edge planes of the
-//             current buffer with both z-neighbours (RCCL or D2D), record evC;
-//   stream A: step 0 on the planes that need no ghost, [1, nz-1), overlapped
-//             with the exchange; then (after evC) step 0 on the rim
-//             [-(g-1), 1) u [nz-1, nz+g-1); then steps s = 1..g-1 on the
-//             shrinking extended range [-(g-1-s), nz+g-1-s); the last step
-//             computes its edge planes [0, G) u [nz-G, nz) first and records
-//             evE, so the NEXT block's exchange overlaps this step's middle
-//             as well as the next core; record evA.
+// The schedule of a deep-halo block of g <= G steps on a slab of nz planes
+// with a ghost zone of G planes:
+//   EXCHANGE     stream B, after the previous block's EDGES_DONE: G edge planes
+//                of the block's input field to both z-neighbours, their ghosts in;
+//   STEP 0 core  [1, nz-1), the planes that need no ghost: overlaps the exchange;
+//   WAIT_EXCHANGE, STEP 0 rim [-(g-1), 1) u [nz-1, nz+g-1) (one launch);
+//   steps 1 .. g-1 on the shrinking extended range [-(g-1-s), nz+g-1-s): with
+//   fuse2, the steps before the last go in pairs (s, s+1) that write step
+//   s+1's range [-(g-2-s), nz+g-2-s) and read step s-1's, both inside the
+//   ghost zone; the last step computes its edge planes [0, G) u [nz-G, nz)
+//   first and marks EDGES_DONE, so the NEXT block's exchange overlaps this
+//   step's middle as well as the next core.
 // Ghost-zone sites are recomputed redundantly; the counter-based noise makes
 // them bit-identical to their owner's, so the result equals the monolithic run.
+std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first) {
+    std::vector<sq_block_op> ops;
+    auto add = [&](int kind, int step, int lo, int hi, int lo2 = 0, int hi2 = 0) {
+        ops.push_back(sq_block_op{kind, step, lo, hi, lo2, hi2});
+    };
+    add(SQ_OP_EXCHANGE, 0, 0, 0);
+    if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1);
+    add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
+    const int lo_a = -(g - 1), hi_a = 1, lo_b = nz - 1, hi_b = nz + g - 1;
+    if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
+        add(SQ_OP_STEP, 0, lo_a, hi_b);
+    else
+        add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b);
+    bool edges = false;
+    for (int st = 1; st < g;) {
+        if (fuse2 && st + 1 < g - 1) {
+            const int e = g - 2 - st;  // ghost planes step st+1 still updates on either side
+            add(SQ_OP_PAIR, st, -e, nz + e);
+            st += 2;
+            continue;
+        }
+        if (st == g - 1 && edge_first && nz > 2 * G) {
+            add(SQ_OP_STEP, st, 0, G);
+            add(SQ_OP_STEP, st, nz - G, nz);
+            add(SQ_OP_EDGES_DONE, st, 0, 0);
+            add(SQ_OP_STEP, st, G, nz - G);
+            edges = true;
+        } else {
+            add(SQ_OP_STEP, st, -(g - 1 - st), nz + (g - 1 - st));
+        }
+        ++st;
+    }
+    if (!edges) add(SQ_OP_EDGES_DONE, g - 1, 0, 0);
+    return ops;
+}
+
+// Deep-halo block of g <= gz steps on every slab: executes block_plan.
 int phi4_block(sq_ctx *c, int g) {
     const size_t plane = plane_floats(c);
     const int ns = (int)c->slabs.size(), G = c->gz;
     const size_t gbytes = (size_t)G * plane * sizeof(float);
     const int cur = c->cur;
-    // 1. exchange (stream B)
+    const unsigned long long step0 = c->step;
+    // 1. exchange (stream B), for every slab before any slab waits for one
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
         SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
@@ -423,76 +410,58 @@ int phi4_block(sq_ctx *c, int g) {
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     }
-    // 2. step 0, ghost-free core (overlaps the exchange)
-    for (auto &s : c->slabs) {
-        int rc = phi4_launch_span(c, s, cur, s.sA, 1, s.nz - 1, true);
-        if (rc) return rc;
-    }
-    // 3. step 0 rim, after the ghosts arrived and our own sends left
+    // 2. the rest of the schedule, slab by slab (each slab has its own stream A;
+    //    slabs of a loopback decomposition may differ in nz, hence in schedule)
+    int out_buf = cur;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        SQ_HIP(hipStreamWaitEvent(s.sA, s.evC, 0));
-        if (c->p.comm == SQ_COMM_LOOPBACK) {
-            SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
-            SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
-        }
-        const int lo_a = -(g - 1), hi_a = 1, lo_b = s.nz - 1, hi_b = s.nz + g - 1;
-        int rc;
-        if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
-            rc = phi4_launch_span(c, s, cur, s.sA, lo_a, hi_b, false);
-        else
-            rc = phi4_launch_range(c, s, cur, s.sA, lo_a, hi_b, lo_b - lo_a, g, 2, 0, false);
-        if (rc) return rc;
-    }
-    count_step(c);
-    // 4. steps 1..g-1 on the shrinking extended range; the last one edges
-    //    first.  With the two-step kernel (tbz > 0) the steps before the last
-    //    go in pairs: the pair (st, st+1) writes step st+1's range and reads
-    //    step st-1's, both inside the ghost zone; ib tracks the buffer that
-    //    holds the latest step (a pair flips it once, not twice).
-    std::vector<char> edges_recorded(c->slabs.size(), 0);  // per slab: slabs of a decomposition differ in nz
-    int ib = cur ^ 1;
-    for (int st = 1; st < g;) {
-        if (c->tbz > 0 && st + 1 < g - 1) {
-            const int e = g - 2 - st;  // ghost planes step st+1 still updates on either side
-            for (auto &s : c->slabs) {
-                int rc = phi4_tb2_range(c, s, ib, s.sA, -e, s.nz + e, 0, true);
-                if (rc) return rc;
+        const std::vector<sq_block_op> ops = block_plan(s.nz, G, g, c->tbz > 0, c->edge_first);
+        int in = cur;            // buffer holding the latest completed step
+        bool flip = false;       // a STEP op of the current step wrote in ^ 1
+        int last = -1;           // step of the previous STEP op
+        for (const sq_block_op &op : ops) {
+            int rc = SQ_OK;
+            switch (op.kind) {
+            case SQ_OP_EXCHANGE: break;  // issued above for every slab
+            case SQ_OP_WAIT_EXCHANGE:
+                SQ_HIP(hipStreamWaitEvent(s.sA, s.evC, 0));
+                if (c->p.comm == SQ_COMM_LOOPBACK) {
+                    SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
+                    SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
+                }
+                break;
+            case SQ_OP_EDGES_DONE: SQ_HIP(hipEventRecord(s.evE, s.sA)); break;
+            case SQ_OP_STEP: {
+                if (op.step != last && flip) in ^= 1;
+                const bool first = op.step != last;  // the first launch of a step carries its timing
+                flip = true;
+                last = op.step;
+                c->step = step0 + (unsigned long long)op.step;
+                if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
+                    rc = phi4_launch_range(c, s, in, s.sA, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
+                else
+                    rc = phi4_launch_span(c, s, in, s.sA, op.lo, op.hi, first);
+                break;
             }
-            ib ^= 1;
-            count_step(c);
-            count_step(c);
-            st += 2;
-            continue;
-        }
-        const int in_buf = ib;
-        const bool split = st == g - 1;
-        for (size_t i = 0; i < c->slabs.size(); ++i) {
-            Slab &s = c->slabs[i];
-            int rc;
-            if (split && c->edge_first && s.nz > 2 * G) {
-                rc = phi4_launch_span(c, s, in_buf, s.sA, 0, G, true);
-                if (rc) return rc;
-                rc = phi4_launch_span(c, s, in_buf, s.sA, s.nz - G, s.nz, false);
-                if (rc) return rc;
-                SQ_HIP(hipEventRecord(s.evE, s.sA));
-                rc = phi4_launch_span(c, s, in_buf, s.sA, G, s.nz - G, false);
-                edges_recorded[i] = 1;
-            } else {
-                rc = phi4_launch_span(c, s, in_buf, s.sA, -(g - 1 - st), s.nz + (g - 1 - st), true);
+            case SQ_OP_PAIR:
+                if (flip) in ^= 1;
+                flip = false;
+                last = op.step + 1;
+                c->step = step0 + (unsigned long long)op.step;
+                rc = phi4_tb2_range(c, s, in, s.sA, op.lo, op.hi, 0, true);
+                in ^= 1;
+                break;
+            default: return fail(SQ_E_STATE, "unknown block op");
             }
             if (rc) return rc;
         }
-        ib ^= 1;
-        count_step(c);
-        ++st;
-    }
-    for (size_t i = 0; i < c->slabs.size(); ++i) {
-        Slab &s = c->slabs[i];
+        if (flip) in ^= 1;
         SQ_HIP(hipEventRecord(s.evA, s.sA));
-        if (!edges_recorded[i]) SQ_HIP(hipEventRecord(s.evE, s.sA));
+        out_buf = in;
     }
-    c->cur = ib;
+    c->step = step0;
+    for (int k = 0; k < g; ++k) count_step(c);
+    c->cur = out_buf;
     return SQ_OK;
 }
 
@@ -542,17 +511,13 @@ int phi4_autotune(sq_ctx *c, int &n) {
         SQ_HIP(hipMemcpyAsync(ms.data(), c->dtune, sizeof(double) * ms.size(), hipMemcpyDeviceToHost, st));
         SQ_HIP(hipStreamSynchronize(st));
     }
-    size_t best = 0;
-    for (size_t k = 1; k < cand.size(); ++k)
-        if (ms[k] < ms[best]) best = k;
-    c->gz = cand[best];
+    c->gz = cand[(size_t)sq_phi4_pick_ghost(ms.data(), (int)ms.size())];
     c->g_tuned = true;
     return SQ_OK;
 }
 
 int phi4_steps(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
-        if (c->pblocks > 0) return n > 0 ? phi4_persist_steps(c, n) : SQ_OK;
         for (; c->tbz > 0 && n >= 2; n -= 2) {
             int rc = phi4_tb2_pair(c);
             if (rc) return rc;
@@ -580,12 +545,6 @@ int phi4_join(sq_ctx *c) {
     for (auto &s : c->slabs) {
         SQ_HIP(hipStreamSynchronize(s.sA));
         SQ_HIP(hipStreamSynchronize(s.sB));
-    }
-    if (c->ppending) {
-        c->ppending = false;
-        int e = 0;
-        SQ_HIP(hipMemcpy(&e, c->perr, sizeof(int), hipMemcpyDeviceToHost));
-        if (e) return fail(SQ_E_HIP, "persistent step kernel: a dependency wait timed out");
     }
     return SQ_OK;
 }
@@ -621,7 +580,10 @@ int create_phi4(sq_ctx *c) {
         const double field_bytes = 4.0 * c->Lx * c->Ly * (double)nz_dev;  // this device's share
         if (c->geom.pf == 7 && 2.0 * field_bytes > 2.0 * (1 << 30)) c->geom.pf = 4;
     }
-    if (const char *e = getenv("SQ_PREFETCH")) c->geom.pf = (atoi(e) >= 1 && atoi(e) <= 7) ? atoi(e) : 1;
+    if (const char *e = getenv("SQ_PREFETCH")) {  // tuning override of the store / arithmetic mode
+        const int m = atoi(e);
+        c->geom.pf = (m == 3 || m == 4 || m == 7) && c->geom.qx == 64 ? m : 1;
+    }
     int nslab = 1;
     long long zfirst = 0;
     std::vector<long long> zs;
@@ -715,9 +677,6 @@ int create_phi4(sq_ctx *c) {
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
     c->zc = zc;
-    // Opt-in (SQ_PERSIST=1): bit-identical, but measured 55 us per 256^3 step
-    // (31 us with the dependency waits removed) vs 21.5 us for per-step
-    // launches (profiles/r01/persist_ab.log).
     // Two steps per launch on 256-wide lattices (SQ_FUSE2=0: off; SQ_FUSE2_Z:
     // pin the output planes per block), single slab and deep-halo slabs alike.
     // 256^3: 19.5 vs 22.0 us per step on the same box; one round of two
@@ -740,33 +699,6 @@ int create_phi4(sq_ctx *c) {
         int ncu = 0;
         SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
         c->tb_blocks = 2 * std::max(1, ncu);  // 68 VGPRs, 10 waves: two blocks per CU
-    }
-    const char *pe = getenv("SQ_PERSIST");
-    if (p.comm == SQ_COMM_NONE && pe && atoi(pe) != 0) {
-        const int nxseg = c->Lx / (4 * c->geom.qx * c->geom.v);
-        const int nzc = (c->slabs[0].nz + zc - 1) / zc;
-        const long long nunits = (long long)nxseg * ((c->Ly + c->geom.wy - 1) / c->geom.wy) * nzc;
-        int ncu = 0;
-        SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
-        const long long cap = 4ll * sq::phi4_persist_blocks(c->geom, nxseg > 1, true, ncu);
-        int umin = 1;
-        if (const char *e = getenv("SQ_PERSIST_U")) umin = std::max(1, atoi(e));
-        // the fewest units per wave (most waves) that fit co-resident, with the
-        // same count for every wave and whole blocks on every XCD
-        int U = 0;
-        for (int u = umin; u <= nzc && U == 0; ++u)
-            if (nzc % u == 0 && (nunits / u) % 32 == 0 && nunits / u <= cap) U = u;
-        if (U > 0 && nunits < (1ll << 30)) {
-            c->tbz = 0;  // the persistent launches replace the two-step fusion
-            c->pU = U;
-            c->pblocks = (int)(nunits / U / 4);
-            c->pdone_bytes = sizeof(unsigned int) * (size_t)nunits;
-            SQ_HIP(hipMalloc(&c->pdone, c->pdone_bytes));
-            SQ_HIP(hipMemset(c->pdone, 0, c->pdone_bytes));
-            SQ_HIP(hipMalloc(&c->perr, sizeof(int)));
-            SQ_HIP(hipMemset(c->perr, 0, sizeof(int)));
-            if (const char *e = getenv("SQ_PERSIST_STEPS")) c->pchunk = std::max(1, atoi(e));
-        }
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
@@ -1125,8 +1057,6 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->dacc);
     (void)hipFree(c->dtune);
     (void)hipFree(c->dmax);
-    (void)hipFree(c->pdone);
-    (void)hipFree(c->perr);
     if (c->qstream) (void)hipStreamDestroy(c->qstream);
     for (auto &e : c->evpool) {
         (void)hipEventDestroy(e.a);
@@ -1299,20 +1229,12 @@ int sq_phi4_kernel(sq_ctx *c, char *name, size_t cap) {
     // (rocprofv3 prints the kernel under exactly this name)
     const bool ms = c->Lx / (4 * c->geom.qx * c->geom.v) > 1;
     const bool nz = (float)(sqrt(2.0 * (double)(float)c->dtau) * c->p.C) != 0.0f;
-    int pf = c->geom.pf;
-    if (pf == 2 && !(c->geom.qx == 64 && c->geom.v == 1)) pf = 1;
-    if (pf >= 3 && c->geom.qx != 64) pf = 1;
-    if (pf == 5 && ms) pf = 3;
+    const int pf = c->geom.pf;
     if (c->tbz > 0 && c->tbz_pin)
         snprintf(name, cap, "phi4_tb2_kernel<%s> (2 steps per launch) z=%d", nz ? "true" : "false", c->tbz);
     else if (c->tbz > 0)
         snprintf(name, cap, "phi4_tb2_kernel<%s> (2 steps per launch) one round of %d blocks", nz ? "true" : "false",
                  c->tb_blocks);
-    else if (c->pblocks > 0)
-        snprintf(name, cap,
-                 "phi4_persist_kernel<%d, %d, %d, %s, %s> zc=%d, <= %d steps per launch, %d blocks, %d units per wave",
-                 c->geom.qx, c->geom.r, c->geom.v, ms ? "true" : "false", nz ? "true" : "false", c->zc, c->pchunk,
-                 c->pblocks, c->pU);
     else
         snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d> zc=%d", c->geom.qx, c->geom.r, c->geom.v,
                  ms ? "true" : "false", nz ? "true" : "false", pf, c->zc);
@@ -1325,6 +1247,24 @@ int sq_phi4_ghost(sq_ctx *c, int *active, int *allocated) {
     if (active) *active = c->p.comm == SQ_COMM_NONE ? 0 : c->gz;
     if (allocated) *allocated = c->p.comm == SQ_COMM_NONE ? 0 : c->gpad;
     return SQ_OK;
+}
+
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
+                       int *nops) {
+    if (!nops || (cap > 0 && !ops)) return fail(SQ_E_ARG, "null argument");
+    if (nz < 1 || ghost < 1 || g < 1 || g > ghost || ghost > nz) return fail(SQ_E_ARG, "need 1 <= g <= ghost <= nz");
+    const std::vector<sq_block_op> v = block_plan(nz, ghost, g, fuse2 != 0, edge_first != 0);
+    *nops = (int)v.size();
+    if ((int)v.size() > cap) return fail(SQ_E_ARG, "cap too small: need " + std::to_string(v.size()));
+    std::copy(v.begin(), v.end(), ops);
+    return SQ_OK;
+}
+
+int sq_phi4_pick_ghost(const double *ms, int n) {
+    int best = 0;
+    for (int k = 1; k < n; ++k)
+        if (ms[k] < ms[best]) best = k;
+    return best;
 }
 
 int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {

@@ -35,30 +35,11 @@ struct Phi4Geom {
     int qx;   // lanes per x segment (4 sites each)
     int r;    // rows per lane
     int wy;   // rows per wave unit
-    int pf;   // register queue: 1 prefetch distance 1; 2 distance 2 (qx == 64, v == 1);
-              // 3 distance 1 + packed-f32 site arithmetic (qx == 64, the default there);
-              // 4 as 3 with non-temporal output stores (default above 2 GiB of fields per device);
-              // 5 as 3 with LDS-staged y-halo rows; 6 / 7 as 3 with sc1 / sc0 sc1 output
-              // stores (7: the default for full-row waves)
+    int pf;   // store / arithmetic mode: 1 scalar site arithmetic (narrow rows); 3 packed-f32 site
+              // arithmetic (qx == 64); 4 as 3 with non-temporal output stores (default above 2 GiB
+              // of fields per device); 7 as 3 with sc0 sc1 output stores (default for full-row waves)
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
-
-// Persistent multi-step launch (single periodic slab): every wave owns U units
-// and runs them step after step, starting a unit as soon as the units it
-// reads have completed the previous step (dataflow, no kernel boundary
-// between steps).
-struct Phi4PersistArgs {
-    Phi4StepArgs a[2];    // step s of the launch: a[s & 1] (in / out swapped; a[0].in = the first input)
-    unsigned int *done;   // per unit: stamp of its last completed step
-    int *err;             // set to 1 when a dependency wait timed out
-    unsigned int base;    // stamp of the last step completed before this launch
-    int nsteps;
-    int U, nzq;           // units per wave (z-chunks nzq = nzc / U apart); waves = nunits / U
-};
-// Blocks of the persistent launch for this geometry (all co-resident,
-// multiple of 8), 0 if it has no persistent variant.
-int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu);
-hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s);
 
 // Two steps per launch (steps s and s+1, s = a.s_hi:a.s_lo) on planes
 // [a.zlo, a.zhi) (a single periodic slab: [0, nz)): a.zc = output planes per

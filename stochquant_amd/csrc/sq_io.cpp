@@ -10,6 +10,7 @@
 // which callers may apply).
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <vector>
 
@@ -43,9 +44,14 @@ bool write_npy(const char *path, const float *data, long long nz, long long ny, 
     return fclose(fp) == 0 && ok;
 }
 
-bool read_npy(const char *path, std::vector<float> &out, long long shape[3]) {
+// Reads a float32 C-order .npy whose shape must equal want[3]; the header is
+// checked before anything is allocated (a corrupt or foreign file fails here).
+bool read_npy(const char *path, std::vector<float> &out, const long long want[3], std::string *why) {
     FILE *fp = fopen(path, "rb");
-    if (!fp) return false;
+    if (!fp) {
+        *why = "cannot open";
+        return false;
+    }
     unsigned char head[10];
     bool ok = fread(head, 1, 10, fp) == 10 && head[0] == 0x93 && memcmp(head + 1, "NUMPY", 5) == 0 &&
               head[6] == 1;
@@ -57,15 +63,42 @@ bool read_npy(const char *path, std::vector<float> &out, long long shape[3]) {
     }
     ok = ok && hdr.find("'<f4'") != std::string::npos && hdr.find("'fortran_order': False") != std::string::npos;
     const size_t sp = ok ? hdr.find("'shape': (") : std::string::npos;
+    long long shape[3] = {-1, -1, -1};
     ok = ok && sp != std::string::npos &&
          sscanf(hdr.c_str() + sp + 10, "%lld, %lld, %lld", &shape[0], &shape[1], &shape[2]) == 3;
+    if (!ok) {
+        *why = "not a float32 C-order 3-D .npy";
+    } else if (shape[0] != want[0] || shape[1] != want[1] || shape[2] != want[2]) {
+        *why = "shape (" + std::to_string(shape[0]) + ", " + std::to_string(shape[1]) + ", " +
+               std::to_string(shape[2]) + ") does not match this slab (" + std::to_string(want[0]) + ", " +
+               std::to_string(want[1]) + ", " + std::to_string(want[2]) + ")";
+        ok = false;
+    }
     if (ok) {
-        const size_t n = (size_t)(shape[0] * shape[1] * shape[2]);
+        const size_t n = (size_t)(want[0] * want[1] * want[2]);
         out.resize(n);
         ok = fread(out.data(), sizeof(float), n, fp) == n;
+        if (!ok) *why = "truncated data";
     }
     fclose(fp);
     return ok;
+}
+
+bool read_text(const std::string &path, std::string *j) {
+    FILE *fp = fopen(path.c_str(), "r");
+    if (!fp) return false;
+    char buf[512];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, fp)) > 0 && j->size() < (1u << 16)) j->append(buf, n);
+    fclose(fp);
+    return true;
+}
+
+bool json_dims(const std::string &j, long long d[3]) {
+    const size_t p = j.find("\"dims\":");
+    if (p == std::string::npos) return false;
+    const size_t b = j.find('[', p);
+    return b != std::string::npos && sscanf(j.c_str() + b + 1, "%lld , %lld , %lld", &d[0], &d[1], &d[2]) == 3;
 }
 
 long long json_int(const std::string &j, const char *key, bool *found) {
@@ -86,8 +119,7 @@ double json_dbl(const std::string &j, const char *key, bool *found) {
 
 extern "C" {
 
-int sq_save_field(sq_ctx *ctx, const char *path) {
-    if (!ctx || !path) return io_fail("null argument");
+static int save_field(sq_ctx *ctx, const char *path) {
     int tile[4];
     if (sq_phi4_tile(ctx, tile) != SQ_OK) return io_fail("sq_save_field: PHI4 contexts only");
     long long nz = 0, z0 = 0;
@@ -112,40 +144,71 @@ int sq_save_field(sq_ctx *ctx, const char *path) {
     return fclose(fp) == 0 ? SQ_OK : io_fail("cannot write " + jpath);
 }
 
-int sq_load_field(sq_ctx *ctx, const char *path, int restore_counters) {
+int sq_save_field(sq_ctx *ctx, const char *path) {
     if (!ctx || !path) return io_fail("null argument");
+    try {
+        return save_field(ctx, path);
+    } catch (const std::exception &e) {
+        return io_fail(std::string("sq_save_field: ") + e.what());
+    } catch (...) {
+        return io_fail("sq_save_field: unexpected exception");
+    }
+}
+
+// Validates everything (the .npy header against this slab, the metadata's
+// dims / z0 / seed) before the device field is touched, so a failed load
+// leaves the context's state as it was.
+static int load_field(sq_ctx *ctx, const char *path, int restore_counters) {
     int tile[4];
     if (sq_phi4_tile(ctx, tile) != SQ_OK) return io_fail("sq_load_field: PHI4 contexts only");
     long long nz = 0, z0 = 0;
     sq_slab(ctx, &nz, &z0);
     sq_params P;
     if (sq_get_params(ctx, &P) != SQ_OK) return io_fail("sq_get_params failed");
+    const std::string jpath = std::string(path) + ".json";
+    std::string j;
+    const bool have_meta = read_text(jpath, &j);
+    if (restore_counters && !have_meta) return io_fail("cannot read " + jpath);
+    long long step = 0, jz0 = 0, jnz = 0;
+    double dtau = 0;
+    if (have_meta) {
+        bool f1, f2, f3, f4, f5;
+        step = json_int(j, "step", &f1);
+        dtau = json_dbl(j, "dtau", &f2);
+        jz0 = json_int(j, "z0", &f3);
+        jnz = json_int(j, "nz", &f4);
+        const unsigned long long seed = (unsigned long long)json_int(j, "seed", &f5);
+        long long dims[3];
+        if (!f1 || !f2 || !f3 || !f4 || !f5 || !json_dims(j, dims)) return io_fail("incomplete checkpoint metadata " + jpath);
+        if (dims[0] != P.dims[0] || dims[1] != P.dims[1] || dims[2] != P.dims[2])
+            return io_fail("checkpoint lattice dims do not match this context");
+        if (jz0 != z0 || jnz != nz) return io_fail("checkpoint z0 / nz do not match this slab");
+        // continuing the noise stream needs the same Philox key
+        if (restore_counters && seed != P.seed) return io_fail("checkpoint seed does not match this context");
+        if (restore_counters && !(dtau > 0)) return io_fail("checkpoint dtau must be > 0");
+    }
     std::vector<float> f;
-    long long shape[3];
-    if (!read_npy(path, f, shape)) return io_fail(std::string("cannot read .npy float32 field ") + path);
-    if (shape[0] != nz || shape[1] != P.dims[1] || shape[2] != P.dims[0])
-        return io_fail("checkpoint shape does not match this slab");
+    const long long want[3] = {nz, P.dims[1], P.dims[0]};
+    std::string why;
+    if (!read_npy(path, f, want, &why)) return io_fail(std::string("cannot read field ") + path + ": " + why);
     int rc = sq_upload_field(ctx, f.data(), f.size());
     if (rc) return rc;
     if (restore_counters) {
-        const std::string jpath = std::string(path) + ".json";
-        FILE *fp = fopen(jpath.c_str(), "r");
-        if (!fp) return io_fail("cannot read " + jpath);
-        std::string j;
-        char buf[512];
-        size_t n;
-        while ((n = fread(buf, 1, sizeof buf, fp)) > 0) j.append(buf, n);
-        fclose(fp);
-        bool f1, f2, f3;
-        const long long step = json_int(j, "step", &f1);
-        const double dtau = json_dbl(j, "dtau", &f2);
-        const long long jz0 = json_int(j, "z0", &f3);
-        if (!f1 || !f2 || !f3) return io_fail("incomplete checkpoint metadata " + jpath);
-        if (jz0 != z0) return io_fail("checkpoint z0 does not match this slab");
         sq_set_step(ctx, (unsigned long long)step);
         sq_set_dtau(ctx, dtau);
     }
     return SQ_OK;
+}
+
+int sq_load_field(sq_ctx *ctx, const char *path, int restore_counters) {
+    if (!ctx || !path) return io_fail("null argument");
+    try {  // no exception crosses the C ABI (std::bad_alloc on a huge slab, ...)
+        return load_field(ctx, path, restore_counters);
+    } catch (const std::exception &e) {
+        return io_fail(std::string("sq_load_field: ") + e.what());
+    } catch (...) {
+        return io_fail("sq_load_field: unexpected exception");
+    }
 }
 
 }  // extern "C"

@@ -157,23 +157,20 @@ struct Lane {
     uint32_t qoff[R * V];   // Philox quad offset inside the plane
     bool rows_ok;
     int lane;
-    int w;                  // wave in the block
-    int hmask;              // halo rows this wave loads from memory: bit 0 y-1, bit 1 y+R
-    float4 *lds;            // LH: the block's boundary-row exchange buffer
 };
 
-template <int QX, int R, int V, int LAUX = 0>
+template <int QX, int R, int V>
 __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                           Slot<R, V> &s, int zl, bool halo, size_t plane,
                                           uint32_t pbytes) {
     const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, zl), plane, pbytes);
 #pragma unroll
-    for (int k = 0; k < R * V; ++k) s.row[k] = bload4<LAUX>(rs, L.voff[k]);
+    for (int k = 0; k < R * V; ++k) s.row[k] = bload4(rs, L.voff[k]);
     if (halo) {
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-            if (L.hmask & 1) s.hm[v] = bload4<LAUX>(rs, L.vm[v]);
-            if (L.hmask & 2) s.hp[v] = bload4<LAUX>(rs, L.vp[v]);
+            s.hm[v] = bload4(rs, L.vm[v]);
+            s.hp[v] = bload4(rs, L.vp[v]);
         }
     }
 }
@@ -182,7 +179,7 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false, int LAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
@@ -194,8 +191,8 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         for (int r = 0; r < R; ++r) {
             el[r] = 0.f;
             er[r] = 0.f;
-            if (L.lane == 0) el[r] = bload1<LAUX>(rs, L.vl[r]);
-            if (L.lane == 63) er[r] = bload1<LAUX>(rs, L.vr[r]);
+            if (L.lane == 0) el[r] = bload1(rs, L.vl[r]);
+            if (L.lane == 63) er[r] = bload1(rs, L.vr[r]);
         }
     }
     // noise for the R*V float4s of plane z: independent of the loads in flight
@@ -215,35 +212,11 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 #pragma unroll
         for (int k = 0; k < R * V; ++k) xi[k] = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
-    // y-halo rows: from memory, or (LH, queue mode 5, SQ_PREFETCH=5) the 4 y-adjacent waves of the block
-    // publish their first / last rows in LDS and only the block's two outer
-    // halo rows come from memory (double-buffered by plane parity: one barrier
-    // per plane keeps the waves within one plane of each other).  Measured
-    // (profiles/r01/sweep*_lds_halo.log): halves the L2 requests but the
-    // per-plane barrier costs more than the L2 hits it saves -- 256^3 20.8 ->
-    // 21.6 us, 512^3 unchanged -- so the default reads halos from L2.
     float4 hmv[V], hpv[V];
-    if constexpr (LH) {
-        float4 *mine = L.lds + ((z & 1) * 4 + L.w) * 2 * V * 64;
 #pragma unroll
-        for (int v = 0; v < V; ++v) {
-            mine[v * 64 + L.lane] = C.row[v];
-            mine[(V + v) * 64 + L.lane] = C.row[(R - 1) * V + v];
-        }
-        __syncthreads();
-        const float4 *up_w = L.lds + ((z & 1) * 4 + L.w - 1) * 2 * V * 64;
-        const float4 *dn_w = L.lds + ((z & 1) * 4 + L.w + 1) * 2 * V * 64;
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            hmv[v] = L.w == 0 ? C.hm[v] : up_w[(V + v) * 64 + L.lane];
-            hpv[v] = L.w == 3 ? C.hp[v] : dn_w[v * 64 + L.lane];
-        }
-    } else {
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            hmv[v] = C.hm[v];
-            hpv[v] = C.hp[v];
-        }
+    for (int v = 0; v < V; ++v) {
+        hmv[v] = C.hm[v];
+        hpv[v] = C.hp[v];
     }
     const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, A.periodic ? z + 1 : z + A.gz, plane, pbytes);
 #pragma unroll
@@ -297,34 +270,19 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0, bool LH = false, int LAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
                                            uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
-    load_slot<QX, R, V, LAUX>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
-}
-
-// Prefetch distance 2: plane z+1 is already in N; load plane z+2 into F (one
-// whole plane of work ahead of its use), then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ>
-__device__ __forceinline__ void plane_step2(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
-                                            const Slot<R, V> &P, const Slot<R, V> &C,
-                                            const Slot<R, V> &N, Slot<R, V> &F, int z, int zend,
-                                            size_t plane, uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
-    if (z + 2 <= zend) load_slot<QX, R, V>(A, L, F, z + 2, z + 2 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, false>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
+    load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
 }
 
 // One wave's unit of a step: an x-span of 4*QX*V sites by R row sets by a
-// z-chunk.  LAUX: cache policy of the field loads (16 = sc1 in the
-// persistent kernel, whose inputs were written by other waves of the same
-// launch: sc1 loads skip the per-CU L1, which other CUs' stores never
-// refresh).
-template <int QX, int R, int V, bool MS, bool NZ, int PF, int LAUX = 0>
-__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4 *lds, int &bad, uint32_t slo,
-                                         uint32_t shi) {
+// z-chunk.
+template <int QX, int R, int V, bool MS, bool NZ, int PF>
+__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, int &bad, uint32_t slo, uint32_t shi) {
     constexpr int RS = 64 / QX;  // row sets per wave
     // x-segments fastest, then y-groups: the waves that share a row's segment
     // edges (MS) and the y-halo rows are consecutive units, i.e. the same or
@@ -342,10 +300,6 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4
     const uint32_t qplane = (uint32_t)(plane >> 2);
     Lane<QX, R, V> L;
     L.lane = threadIdx.x & 63;
-    L.w = (int)(threadIdx.x >> 6);
-    constexpr bool LH = PF == 5;
-    L.lds = lds;
-    L.hmask = LH ? ((L.w == 0 ? 1 : 0) | (L.w == 3 ? 2 : 0)) : 3;
     const int xq = L.lane & (QX - 1);
     const int rsid = L.lane / QX;
     const int xspan = xs * (4 * QX * V);     // first site of this wave's x-span
@@ -378,42 +332,25 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, float4
     }
 
     Slot<R, V> S0, S1, S2;
-    load_slot<QX, R, V, LAUX>(A, L, S0, zbeg - 1, false, plane, pbytes);
-    load_slot<QX, R, V, LAUX>(A, L, S1, zbeg, true, plane, pbytes);
+    load_slot<QX, R, V>(A, L, S0, zbeg - 1, false, plane, pbytes);
+    load_slot<QX, R, V>(A, L, S1, zbeg, true, plane, pbytes);
     int ubad = 0;
-    if constexpr (PF != 2) {
-        // three-slot register queue, unrolled so no rotation moves are needed
-        // (PF == 3: same queue, packed-f32 site arithmetic)
-        constexpr bool PK = PF >= 3;
-        // PF == 4: non-temporal output stores, for lattices whose two fields
-        // exceed the Infinity Cache (the output is not re-read this step, and
-        // keeping it out of L2/MALL leaves them to the input's halo reuse):
-        // 512^3 199.7 -> 186.8 us, 1024^3 1606 -> 1570 us; at 256^3 (MALL-
-        // resident) it costs 21.6 -> 30.0 us (profiles/r01/sweep*_ntstore.log)
-        // PF == 6 / 7: sc1 / sc0 sc1 output stores (write-through that drops
-        // the line from the XCD's L2, guide table "stores of each flavour"), so
-        // the output does not evict the input rows other waves re-read
-        constexpr int SAUX = PF == 4 ? 2 : PF == 6 ? 16 : PF == 7 ? 17 : 0;
-        for (int z = zbeg; z < zend; z += 3) {
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, slo, shi, ubad);
-            if (z + 1 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
-            if (z + 2 >= zend) break;
-            plane_step<QX, R, V, MS, NZ, PK, SAUX, LH, LAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
-        }
-    } else {
-        // four-slot queue, prefetch distance 2
-        Slot<R, V> S3;
-        load_slot<QX, R, V>(A, L, S2, zbeg + 1, zbeg + 1 < zend, plane, pbytes);
-        for (int z = zbeg; z < zend; z += 4) {
-            plane_step2<QX, R, V, MS, NZ>(A, L, S0, S1, S2, S3, z, zend, plane, pbytes, qplane, slo, shi, ubad);
-            if (z + 1 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S1, S2, S3, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
-            if (z + 2 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S2, S3, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
-            if (z + 3 >= zend) break;
-            plane_step2<QX, R, V, MS, NZ>(A, L, S3, S0, S1, S2, z + 3, zend, plane, pbytes, qplane, slo, shi, ubad);
-        }
+    // three-slot register queue, unrolled so no rotation moves are needed.
+    // PF 3: packed-f32 site arithmetic, plain stores; 4: non-temporal output
+    // stores, for lattices whose two fields exceed the Infinity Cache (512^3
+    // 199.7 -> 186.8 us, 1024^3 1606 -> 1570 us; at 256^3 it costs 21.6 ->
+    // 30.0 us, profiles/r01/sw*_ntstore.log); 7: sc0 sc1 (write-through)
+    // output stores, which leave the XCD's L2 at once instead of evicting the
+    // input rows other waves re-read (guide table "stores of each flavour"),
+    // the default for full-row waves.  PF 1: scalar site arithmetic (narrow rows).
+    constexpr bool PK = PF >= 3;
+    constexpr int SAUX = PF == 4 ? 2 : PF == 7 ? 17 : 0;
+    for (int z = zbeg; z < zend; z += 3) {
+        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, slo, shi, ubad);
+        if (z + 1 >= zend) break;
+        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
+        if (z + 2 >= zend) break;
+        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
     }
     if (L.rows_ok) bad |= ubad;
 }
@@ -425,110 +362,10 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
     const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
     if (unit >= A.nunits) return;
-    constexpr bool LH = PF == 5;
-    __shared__ float4 s_halo[LH ? 2 * 4 * 2 * V * 64 : 1];
     int bad = 0;
-    unit_run<QX, R, V, MS, NZ, PF>(A, unit, s_halo, bad, A.s_lo, A.s_hi);
+    unit_run<QX, R, V, MS, NZ, PF>(A, unit, bad, A.s_lo, A.s_hi);
     if (A.flag != nullptr) {
         if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
-    }
-}
-
-// ------------------------------------------------------------ persistent ----
-// All steps of an sq_step call in one launch.  Every wave owns U units of the
-// same x-span and y-group whose z-chunks are nzq = nzc / U apart (c0, c0 +
-// nzq, ...) and runs them in that order, step after step; every wave has the
-// same U, so no wave is a straggler.  A unit of step s waits until the 3 x 3
-// (x 3 with several x-spans) units around it -- the only ones whose planes and
-// rows it reads, and the only ones that read the planes it overwrites -- have
-// completed step s-1.  Those neighbours (z-chunks c +- 1) are, but for the
-// units at a multiple of nzq, units of the same rank i in their own waves,
-// which ran them while this wave ran its units i+1..U-1 of step s-1 and 0..i-1
-// of step s, so the wait is normally already satisfied.  Deadlock freedom:
-// the (step, rank) pairs are ordered, every dependency is on a smaller pair,
-// and all waves are resident (cooperative launch), so the smallest
-// unfinished unit can always run.
-// XCD locality: block b runs on XCD b % 8 and the waves of XCD x are the
-// consecutive wave ids g in [x WX, (x+1) WX), x-span fastest, then y-group,
-// then c0, so an XCD holds whole planes of y-groups and their halo rows.
-// Hand-off (MI355X_MICROARCH.md "Valid forms"): the field is stored with
-// sc0 sc1 (write-through) stores, each wave waits for its stores
-// (vmcnt(0)) before one lane stamps done[unit] (agent-scope store); the
-// consumer polls the stamps with agent-scope loads and reads the field with
-// sc1 loads only, which never hit the per-CU L1.
-constexpr int kPersistSpin = 1 << 21;  // polls before a wait is declared stuck (~seconds)
-
-__device__ __forceinline__ bool wait_deps(const Phi4PersistArgs &P, int xs, int yg, int zk, int unit,
-                                          unsigned need) {
-    const Phi4StepArgs &A = P.a[0];
-    const int lane = threadIdx.x & 63;
-    int dep = unit;
-    if (lane < 27) {
-        int nx = xs + lane % 3 - 1, ny = yg + (lane / 3) % 3 - 1, nzk = zk + lane / 9 - 1;
-        nx = nx < 0 ? A.nxseg - 1 : (nx >= A.nxseg ? 0 : nx);
-        ny = ny < 0 ? A.nyg - 1 : (ny >= A.nyg ? 0 : ny);
-        nzk = nzk < 0 ? A.nzc - 1 : (nzk >= A.nzc ? 0 : nzk);
-        dep = (nzk * A.nyg + ny) * A.nxseg + nx;
-    }
-    for (int it = 0; it < kPersistSpin; ++it) {
-        const unsigned v = __hip_atomic_load(&P.done[dep], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__ballot((int)(v - need) < 0) == 0ull) {
-            __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no field load moves above the poll
-            return true;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-    return false;
-}
-
-// Step s of a persistent launch: this wave's U units in rank order.  False
-// when a dependency wait timed out (the error is flagged; the wave exits).
-typedef const __attribute__((address_space(4))) Phi4StepArgs *KArgs;
-template <int QX, int R, int V, bool MS, bool NZ>
-__device__ __forceinline__ bool persist_step(const Phi4PersistArgs &P, KArgs pa, int s, unsigned long long s0,
-                                             int xs, int yg, int c0, int &bad) {
-    const unsigned long long st = s0 + (unsigned long long)s;
-    for (int i = 0; i < P.U; ++i) {
-        // the unit's argument block is read from the kernarg segment through a
-        // pointer the compiler cannot see through, so nothing derived from it
-        // is hoisted out of the unit / step loops and held in SGPRs across
-        // iterations (hoisting spilled 41-137 SGPRs)
-        KArgs q = pa;
-        asm volatile("" : "+s"(q));
-        const Phi4StepArgs &A = *(const Phi4StepArgs *)q;
-        const int zk = c0 + i * P.nzq;
-        const int unit = (zk * A.nyg + yg) * A.nxseg + xs;
-        if (s > 0 && !wait_deps(P, xs, yg, zk, unit, P.base + (unsigned)s)) {
-            if ((threadIdx.x & 63) == 0) atomicOr(P.err, 1);
-            return false;  // the waves waiting on this one time out in turn: the grid drains
-        }
-        unit_run<QX, R, V, MS, NZ, 7, 16>(A, unit, nullptr, bad, (uint32_t)st, (uint32_t)(st >> 32));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if ((threadIdx.x & 63) == 0)
-            __hip_atomic_store(&P.done[unit], P.base + (unsigned)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return true;
-}
-
-// WPE: waves per SIMD the registers are budgeted for (the whole grid must be
-// resident; at 7 the one-row tile keeps its SGPRs at 87-94, under the 97-112
-// band where the occupancy API reads high: MI355X_MICROARCH.md pitfall
-// table; a budget of 8 spilled 60 SGPRs and a VGPR to scratch).
-template <int QX, int R, int V, bool MS, bool NZ, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_persist_kernel(const Phi4PersistArgs P) {
-    const int b = blockIdx.x;
-    const int wxcd = (int)(gridDim.x >> 3) * 4;  // waves per XCD
-    const int g = __builtin_amdgcn_readfirstlane((b & 7) * wxcd + (b >> 3) * 4 + (int)(threadIdx.x >> 6));
-    const int xs = g % P.a[0].nxseg, rest = g / P.a[0].nxseg, yg = rest % P.a[0].nyg, c0 = rest / P.a[0].nyg;
-    const unsigned long long s0 = ((unsigned long long)P.a[0].s_hi << 32) | P.a[0].s_lo;
-    int bad = 0;
-    const KArgs a0 = (KArgs)((const __attribute__((address_space(4))) char *)__builtin_amdgcn_kernarg_segment_ptr() +
-                             offsetof(Phi4PersistArgs, a));
-    for (int s = 0; s < P.nsteps; ++s) {
-        if (!persist_step<QX, R, V, MS, NZ>(P, a0 + (s & 1), s, s0, xs, yg, c0, bad)) return;
-    }
-    if (P.a[0].flag != nullptr) {
-        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(P.a[0].flag, 1);
     }
 }
 
@@ -810,11 +647,6 @@ static hipError_t launch_pf(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hip
 template <int QX, int R, int V, bool MS>
 static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hipStream_t s,
                            hipEvent_t e0, hipEvent_t e1) {
-    if constexpr (QX == 64 && V == 1) {  // the deeper queue is built for full-row, one-segment waves
-        if (pf == 2)
-            return nz ? launch_pf<QX, R, V, MS, true, 2>(a, grid, s, e0, e1)
-                      : launch_pf<QX, R, V, MS, false, 2>(a, grid, s, e0, e1);
-    }
     if constexpr (QX == 64) {
         if (pf == 3)
             return nz ? launch_pf<QX, R, V, MS, true, 3>(a, grid, s, e0, e1)
@@ -822,21 +654,9 @@ static hipError_t launch_v(const Phi4StepArgs &a, int pf, bool nz, dim3 grid, hi
         if (pf == 4)
             return nz ? launch_pf<QX, R, V, MS, true, 4>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 4>(a, grid, s, e0, e1);
-        if (pf == 6)
-            return nz ? launch_pf<QX, R, V, MS, true, 6>(a, grid, s, e0, e1)
-                      : launch_pf<QX, R, V, MS, false, 6>(a, grid, s, e0, e1);
         if (pf == 7)
             return nz ? launch_pf<QX, R, V, MS, true, 7>(a, grid, s, e0, e1)
                       : launch_pf<QX, R, V, MS, false, 7>(a, grid, s, e0, e1);
-        // LH needs each block's 4 waves to be 4 y-adjacent groups of one z-chunk
-        if constexpr (!MS) {
-            if (pf == 5 && a.nxseg == 1 && a.nyg % 4 == 0)
-                return nz ? launch_pf<QX, R, V, MS, true, 5>(a, grid, s, e0, e1)
-                          : launch_pf<QX, R, V, MS, false, 5>(a, grid, s, e0, e1);
-        }
-        if (pf == 5)
-            return nz ? launch_pf<QX, R, V, MS, true, 3>(a, grid, s, e0, e1)
-                      : launch_pf<QX, R, V, MS, false, 3>(a, grid, s, e0, e1);
     }
     return nz ? launch_pf<QX, R, V, MS, true, 1>(a, grid, s, e0, e1)
               : launch_pf<QX, R, V, MS, false, 1>(a, grid, s, e0, e1);
@@ -871,21 +691,6 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
     }
 }
 
-// The persistent variants built: the default full-row tiles (R = 1, V = 1 for
-// 256-wide rows; R = 2, V = 2 for rows that are multiples of 512).
-static const void *persist_fn(const Phi4Geom &g, bool ms, bool nz) {
-    if (g.qx != 64) return nullptr;
-    if (g.r == 1 && g.v == 1 && !ms)
-        return nz ? (const void *)&phi4_persist_kernel<64, 1, 1, false, true, 7>
-                  : (const void *)&phi4_persist_kernel<64, 1, 1, false, false, 7>;
-    if (g.r == 2 && g.v == 2)
-        return ms ? (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, true, true, 3>
-                        : (const void *)&phi4_persist_kernel<64, 2, 2, true, false, 3>)
-                  : (nz ? (const void *)&phi4_persist_kernel<64, 2, 2, false, true, 3>
-                        : (const void *)&phi4_persist_kernel<64, 2, 2, false, false, 3>);
-    return nullptr;
-}
-
 bool phi4_tb2_supported(int Lx, int Ly) { return Lx == 256 && Ly % kTbRows == 0; }
 
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
@@ -899,26 +704,6 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
     return hipLaunchKernel(fn, grid, block, args, 0, s);
-}
-
-int phi4_persist_blocks(const Phi4Geom &g, bool ms, bool nz, int ncu) {
-    const void *fn = persist_fn(g, ms, nz);
-    if (fn == nullptr || g.pf != 7) return 0;
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess) return 0;
-    // The occupancy API reads one block per CU high at 97-112 SGPRs
-    // (MI355X_MICROARCH.md, pitfall table): the one-row kernels stay under it
-    // (WPE 7), the two-row ones are VGPR-bound at 3; bound by both anyway.
-    per_cu = std::min(per_cu, g.r == 1 && g.v == 1 ? 7 : 3);
-    return (per_cu * ncu) & ~7;
-}
-
-hipError_t phi4_persist_launch(const Phi4PersistArgs &p, const Phi4Geom &g, int blocks, hipStream_t s) {
-    const void *fn = persist_fn(g, p.a[0].nxseg > 1, p.a[0].sig != 0.0f);
-    if (fn == nullptr || blocks <= 0 || (blocks & 7)) return hipErrorInvalidValue;
-    Phi4PersistArgs q = p;
-    void *args[] = {&q};
-    return hipLaunchCooperativeKernel(fn, dim3((unsigned)blocks), dim3(256), args, 0, s);
 }
 
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,

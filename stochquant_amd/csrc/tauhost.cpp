@@ -12,13 +12,12 @@
 // on the MI355X.  Differences, all documented in DESIGN.md: `dev` is a HIP
 // device ordinal (taken modulo the device count, since taumain.py hard-codes
 // the OpenCL platform index 2); no tau_kernel.cl is read from the cwd; the
-// kernel is Jacobi-ordered with Philox noise (seeded from the same rand()
-// draw the reference used for its LCG seed, :185; SQ_SEED overrides).
+// kernel runs the reference's own serial order (Gauss-Seidel sweep, its
+// shared-seed LCG seeded from the same rand() draw, :185; SQ_ORDER_SERIAL in
+// stochquant.h) for N <= 4096, and the Jacobi order with Philox noise keyed by
+// that draw above (SQ_ORDER=jacobi forces it; SQ_SEED overrides the key).
 // SQ_MODEL=phi4 (+ SQ_SHAPE, SQ_M2, SQ_LAMBDA) runs the 3-D lattice behind the
 // same arguments (run_phi4 below).
-// SQ_ORDER=serial selects the reference's own serial order instead
-// (Gauss-Seidel sweep, its shared-seed LCG seeded from that same draw;
-// SQ_ORDER_SERIAL in stochquant.h), N <= 4096.
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -32,6 +31,7 @@
 namespace {
 
 std::chrono::steady_clock::time_point t_start;
+constexpr int kSerialMaxN = 4096;  // SQ_ORDER_SERIAL's limit (sq_qm1d_set_ordering)
 
 double absol(double v) { return v <= 0 ? -v : v; }
 
@@ -284,15 +284,28 @@ int main(int argc, char **argv) {
     p.adapt_dtau = 1;
     sq_ctx *ctx = nullptr;
     if (sq_create(&p, &ctx) != SQ_OK) return die("sq_create", nullptr);
+    // The reference's own serial order (its Gauss-Seidel sweep and shared-seed
+    // LCG, seeded from the same rand() draw as the reference, tauhost.c:185) is
+    // the default wherever it is supported (N <= 4096, every taumain.py preset):
+    // it reproduces the reference's trajectory (to 1 ulp of its float
+    // transcendentals) and is also the faster frame at those sizes (DESIGN.md
+    // §4.1).  Larger chains (config C1's 32,768 sites) and SQ_ORDER=jacobi run
+    // the Jacobi / Philox frame.
+    bool serial = N <= kSerialMaxN;
     if (const char *o = getenv("SQ_ORDER")) {
         if (strcmp(o, "serial") == 0) {
-            if (sq_qm1d_set_ordering(ctx, SQ_ORDER_SERIAL) != SQ_OK) return die("sq_qm1d_set_ordering", ctx);
-            if (sq_qm1d_set_lcg_seed(ctx, seed) != SQ_OK) return die("sq_qm1d_set_lcg_seed", ctx);
-        } else if (strcmp(o, "jacobi") != 0) {
+            serial = true;
+        } else if (strcmp(o, "jacobi") == 0) {
+            serial = false;
+        } else {
             fprintf(stderr, "tauhost: SQ_ORDER must be jacobi or serial\n");
             sq_destroy(ctx);
             return 1;
         }
+    }
+    if (serial) {
+        if (sq_qm1d_set_ordering(ctx, SQ_ORDER_SERIAL) != SQ_OK) return die("sq_qm1d_set_ordering", ctx);
+        if (sq_qm1d_set_lcg_seed(ctx, seed) != SQ_OK) return die("sq_qm1d_set_lcg_seed", ctx);
     }
     if (sq_upload(ctx, f.data(), x.data(), xx0.data(), omega, recSimlgth) != SQ_OK)
         return die("sq_upload", ctx);

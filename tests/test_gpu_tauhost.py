@@ -1,12 +1,13 @@
 """tauhost.o (the drop-in executable) end to end on the MI355X, against the
 reference's recorded outputs (tests/golden/reference_outputs.json).
 
-What is bit-exact with the reference and why: the stdout/end-file formats,
-the initial state (same unseeded glibc rand() draws, tauhost.c:84-102), the
-first printed frame (xavg = 0 -> all -inf), the Δτ controller sequence of the
-all-unstable preset, omega for potID 0 (K = 0 so it never moves), and the
-trailer lines.  The site values after stable frames come from a different
-(counter-based, Jacobi) noise stream and are checked statistically/by format.
+By default (N <= 4096) tauhost.o runs the reference's own serial order with
+its LCG seeded from the same rand() draw, so its trajectory reproduces the
+reference's to the 1-ulp budget of the float transcendentals; the formats,
+initial state (same unseeded glibc rand() draws, tauhost.c:84-102), first
+printed frame (xavg = 0 -> all -inf), Δτ controller sequence, omega for potID
+0 and trailer lines are bit-exact.  SQ_ORDER=jacobi (and N > 4096) runs the
+Jacobi / Philox frame, checked statistically against its own exact law.
 """
 import re
 import shutil
@@ -30,9 +31,9 @@ def _run(tmp_path, argv):
     return r.stdout.decode(), end
 
 
-def test_appendix_c_run(gpu, tmp_path):
+def test_appendix_c_run_jacobi(gpu, tmp_path):
     g = golden("reference_outputs.json")["appendix_c_end_file"]
-    out, end = _run(tmp_path, g["argv"])
+    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="jacobi")
     lines = out.split("\n")
     assert lines[0] == g["stdout_first_line"]
     assert re.fullmatch(r"( -?\d+\.\d{20} \|){3} 0\.01000000000000000021 \|  100\.00", lines[1])
@@ -43,9 +44,9 @@ def test_appendix_c_run(gpu, tmp_path):
         assert len(f) == 4 and all(re.fullmatch(HEX, t) for t in f)
 
 
-def test_all_unstable_preset_dtau_sequence(gpu, tmp_path):
+def test_all_unstable_preset_dtau_sequence_jacobi(gpu, tmp_path):
     g = golden("reference_outputs.json")["double_well_all_unstable"]
-    out, end = _run(tmp_path, g["argv"])
+    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="jacobi")
     dt = [ln.split("|")[-2].strip() for ln in out.strip().split("\n")]
     assert dt == g["printed_dtau"]
     tail = end.strip().split("\n")[-3:]
@@ -66,21 +67,22 @@ def test_stable_preset_and_resume(gpu, tmp_path):
     assert int(end2.strip().split("\n")[-2].split("|")[0]) == g["resume_double_count"]["resume_end_N"]
 
 
-def test_plotted_correlator_matches_exact_stationary_value(gpu, tmp_path):
+@pytest.mark.parametrize("order", ["serial", "jacobi"])
+def test_plotted_correlator_matches_exact_stationary_value(gpu, tmp_path, order):
     """The curve taumain.py plots, log|xavg| (xavg = running <X_i X_mid> -
     <X_i><X_mid>, tauhost.c:519-521), from a 60-frame tauhost.o run converges
-    to the exact stationary connected correlator of the Jacobi chain
-    (tests/qm1d_exact.py).  The reference's own ordering has a different
-    O(dtau) stationary law (Gauss-Seidel; checked against its exact value in
-    test_oracle.py), so the two runs are compared with their own exact laws,
-    not with each other.  ~150 independent samples -> 2.5 sigma = 30 %."""
+    to the exact stationary connected correlator of the chain's ordering
+    (tests/qm1d_exact.py): the default serial order (the reference's
+    Gauss-Seidel sweep) and SQ_ORDER=jacobi have different O(dtau) stationary
+    laws, so each run is compared with its own exact law.  ~150 independent
+    samples -> 2.5 sigma = 30 %."""
     from qm1d_exact import stationary_cov
     from stochquant_amd import parse_frame_line
     argv = ["100", "0.1", "0.002", "60", "0", "1", "0", "1", "0", "1000", "0", "end", "17"]
-    out_gpu, _ = _run(tmp_path, argv)
+    out_gpu, _ = _run_env(tmp_path, argv, SQ_ORDER=order)
     y = parse_frame_line(out_gpu.strip().split("\n")[-1].encode())["y"]   # sites 1..N-1
     c = np.exp(y[39:59])                                                    # sites 40..59
-    exact = stationary_cov(100, 0.1, 0.002, "jacobi")[40:60, 50]
+    exact = stationary_cov(100, 0.1, 0.002, "jacobi" if order == "jacobi" else "gs")[40:60, 50]
     assert np.all(np.isfinite(c))
     assert abs(c.mean() - exact.mean()) < 0.3 * exact.mean()
 
@@ -121,12 +123,13 @@ def _hexrows(text, n):
 
 
 def test_serial_order_reproduces_appendix_c(gpu, oracle_mod, tmp_path):
-    """SQ_ORDER=serial: the reference's serial order with its LCG seeded from
-    the same rand() draw.  The recorded end file and the
-    serial oracle's whole end file agree to the 1-ulp xi budget (float log/cos
-    rounding, tests/test_gpu_qm1d_serial.py); stdout, omega, N, deltaTau exact."""
+    """Default order (no SQ_ORDER): the reference's serial order with its LCG
+    seeded from the same rand() draw.  The recorded end file (SURVEY.md
+    Appendix C) and the serial oracle's whole end file agree to the 1-ulp xi
+    budget (float log/cos rounding, tests/test_gpu_qm1d_serial.py); stdout,
+    omega, N, deltaTau exact."""
     g = golden("reference_outputs.json")["appendix_c_end_file"]
-    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="serial")
+    out, end = _run(tmp_path, g["argv"])
     assert out.split("\n")[0] == g["stdout_first_line"]
     el = end.split("\n")
     assert el[4:7] == g["trailer"]
@@ -144,10 +147,10 @@ def test_serial_order_reproduces_appendix_c(gpu, oracle_mod, tmp_path):
 
 
 def test_serial_order_all_unstable_preset(gpu, tmp_path):
-    """The double-well all-unstable preset in serial order: same printed Δτ
-    sequence and end Δτ / N as the reference's recorded run."""
+    """The double-well all-unstable preset in the default (serial) order: same
+    printed Δτ sequence and end Δτ / N as the reference's recorded run."""
     g = golden("reference_outputs.json")["double_well_all_unstable"]
-    out, end = _run_env(tmp_path, g["argv"], SQ_ORDER="serial")
+    out, end = _run(tmp_path, g["argv"])
     dt = [ln.split("|")[-2].strip() for ln in out.strip().split("\n")]
     assert dt == g["printed_dtau"]
     tail = end.strip().split("\n")[-3:]

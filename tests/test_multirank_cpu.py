@@ -1,12 +1,27 @@
-"""World-size-2 (and 3) gloo rehearsal of the slab decomposition on CPU.
+"""Multi-rank CPU rehearsal (gloo, world size 1-3) of the product's deep-halo
+slab exchange.
 
-Each rank owns planes [Lz*r/P, Lz*(r+1)/P) plus two ghost planes, exchanges
-faces with its z-neighbours exactly as the RCCL path does (send top -> up,
-send bottom -> down, recv lower ghost <- down, recv upper ghost <- up;
-periodic wrap), and steps its slab with the oracle's slab update.  After k
-steps the gathered field must equal the single-process run bit for bit: the
-noise is keyed by the global site and step, so the decomposition cannot
-change a single bit (SURVEY.md §4 T5)."""
+Each rank owns planes [Lz*r/P, Lz*(r+1)/P) plus a ghost zone of G planes on
+either side in two padded ping-pong buffers, exactly as create_phi4 lays them
+out, and executes the product's own schedule (`sq_phi4_block_plan`, the list
+phi4_block in csrc/sq_api.cpp runs on the GPU):
+
+* EXCHANGE: the G top planes to rank r+1, the G bottom planes to rank r-1,
+  lower ghosts from r-1, upper ghosts from r+1, in the product's ncclSend /
+  ncclRecv order (with P = 2 both neighbours are the same peer);
+* STEP ranges that shrink through the ghost zone, the step-0 core/rim split,
+  the last step's edge planes first;
+* PAIR: two steps in one launch (phi4_tb2_kernel) over [lo, hi) reading
+  [lo-2, hi+2) -- rehearsed as step s on [lo-1, hi+1) into a scratch slab
+  and step s+1 on [lo, hi);
+* the ghost depth chosen by the max-reduced trial times (one all-reduce, then
+  sq_phi4_pick_ghost on every rank).
+
+Every plane outside what the schedule writes starts as NaN, so a range that
+reads a stale or never-written plane shows up as a clamped site.  After the
+steps the gathered field must equal the single-process oracle run bit for
+bit: the noise is keyed by global site and step, so the decomposition cannot
+change a single bit (SURVEY.md §8e, T5)."""
 import os
 import socket
 
@@ -14,6 +29,9 @@ import numpy as np
 import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+SHAPE = (16, 8, 36)
+DT, M2, LAM, SEED = 0.02, 0.5, 1.0, 11
 
 
 def _free_port():
@@ -24,74 +42,149 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, shape, steps, q):
+def _exchange(bufs, cur, nz, G, world, up, dn):
+    """The product's halo exchange (sq_api.cpp phi4_block, RCCL branch)."""
+    import torch
+    b = bufs[cur]
+    top = torch.from_numpy(b[G + nz - G:G + nz].copy())   # my top G planes -> up
+    bot = torch.from_numpy(b[G:2 * G].copy())             # my bottom G planes -> down
+    lo = torch.empty_like(top)
+    hi = torch.empty_like(top)
+    if world == 1:
+        lo.copy_(top)
+        hi.copy_(bot)
+    else:
+        ops = [dist.P2POp(dist.isend, top, up), dist.P2POp(dist.isend, bot, dn),
+               dist.P2POp(dist.irecv, lo, dn), dist.P2POp(dist.irecv, hi, up)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    b[0:G] = lo.numpy()
+    b[G + nz:G + nz + G] = hi.numpy()
+
+
+def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn):
+    """Execute one block's schedule; returns the buffer holding the result."""
+    inb, flip, last = cur, False, -1
+    for op in plan:
+        k = op["op"]
+        if k == "exchange":
+            _exchange(bufs, cur, nz, G, world, up, dn)
+        elif k == "step":
+            if op["step"] != last and flip:
+                inb ^= 1
+            flip, last = True, op["step"]
+            oracle.phi4_step_range(p, bufs[inb], bufs[inb ^ 1], G, op["lo"], op["hi"], z0, step0 + op["step"])
+            if op["lo2"] < op["hi2"]:
+                oracle.phi4_step_range(p, bufs[inb], bufs[inb ^ 1], G, op["lo2"], op["hi2"], z0,
+                                       step0 + op["step"])
+        elif k == "pair":
+            if flip:
+                inb ^= 1
+            flip, last = False, op["step"] + 1
+            mid = np.full_like(bufs[inb], np.nan)
+            oracle.phi4_step_range(p, bufs[inb], mid, G, op["lo"] - 1, op["hi"] + 1, z0, step0 + op["step"])
+            oracle.phi4_step_range(p, mid, bufs[inb ^ 1], G, op["lo"], op["hi"], z0, step0 + op["step"] + 1)
+            inb ^= 1
+        else:
+            assert k in ("wait_exchange", "edges_done")
+    return inb ^ 1 if flip else inb
+
+
+def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
     sys.path.insert(0, os.path.dirname(here))
     import torch
     import oracle
-    from stochquant_amd.decomp import slab_bounds, neighbours
+    from stochquant_amd.decomp import block_plan, neighbours, pick_ghost, slab_bounds
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        Lx, Ly, Lz = shape
-        p = oracle.phi4_params(shape, 0.02, 0.5, 1.0, 11)
+        Lx, Ly, Lz = SHAPE
+        p = oracle.phi4_params(SHAPE, DT, M2, LAM, SEED)
         full = oracle.phi4_init(p, 0.8)
         z0, z1 = slab_bounds(Lz, world, rank)
         nz = z1 - z0
-        pad = np.zeros((nz + 2, Ly, Lx), np.float32)
-        pad[1:-1] = full[z0:z1]
         up, dn = neighbours(world, rank)
-        for s in range(steps):
-            top = torch.from_numpy(pad[nz].copy())
-            bot = torch.from_numpy(pad[1].copy())
-            lo = torch.empty_like(top)
-            hi = torch.empty_like(top)
-            if world == 1:
-                lo.copy_(top)
-                hi.copy_(bot)
-            else:
-                ops = [dist.P2POp(dist.isend, top, up), dist.P2POp(dist.isend, bot, dn),
-                       dist.P2POp(dist.irecv, lo, dn), dist.P2POp(dist.irecv, hi, up)]
-                for r in dist.batch_isend_irecv(ops):
-                    r.wait()
-            pad[0] = lo.numpy()
-            pad[nz + 1] = hi.numpy()
-            pad[1:-1] = oracle.phi4_step_slab(p, pad, z0, s)
-        gathered = [torch.zeros(1) for _ in range(world)]
-        dist.all_gather_object(gathered, (z0, pad[1:-1].copy()))
+        # ghost-depth trial: per-rank times differ; the max over ranks picks one G everywhere
+        cands = [g for g in (1, 2, 4, 8) if g <= gpad]
+        ms = torch.tensor([1.0 / g + 0.01 * g + 0.001 * ((rank * 7 + i) % 3) for i, g in enumerate(cands)],
+                          dtype=torch.float64)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        G = cands[pick_ghost(ms.tolist())]
+        # padded ping-pong slabs: allocated depth gpad, active depth G (the product keeps
+        # the allocation and uses the first G planes either side); NaN where nothing valid is
+        bufs = [np.full((nz + 2 * G, Ly, Lx), np.nan, np.float32) for _ in range(2)]
+        bufs[0][G:G + nz] = full[z0:z1]
+        cur, done = 0, 0
+        while done < steps:
+            g = min(G, steps - done)
+            plan = block_plan(nz, G, g, fuse2, edge_first)
+            cur = _run_block(oracle, p, plan, bufs, cur, nz, G, z0, done, world, up, dn)
+            done += g
+        gathered = [None for _ in range(world)]
+        dist.all_gather_object(gathered, (z0, G, bufs[cur][G:G + nz].copy()))
         if rank == 0:
             gathered.sort(key=lambda t: t[0])
-            q.put(np.concatenate([g[1] for g in gathered]))
+            q.put(([g[1] for g in gathered], np.concatenate([g[2] for g in gathered])))
     finally:
         dist.destroy_process_group()
 
 
-def _monolithic(shape, steps):
+def _monolithic(steps):
     import oracle
-    p = oracle.phi4_params(shape, 0.02, 0.5, 1.0, 11)
+    p = oracle.phi4_params(SHAPE, DT, M2, LAM, SEED)
     phi = oracle.phi4_init(p, 0.8)
     for s in range(steps):
         phi = oracle.phi4_step(p, phi, s)
     return phi
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_slab_exchange_bitwise(world, oracle_mod):
-    shape, steps = (16, 8, 12), 4
+@pytest.mark.parametrize("world,steps,fuse2,edge_first,gpad", [
+    (2, 11, True, True, 4),    # P = 2: both neighbours the same peer; partial last block (11 = 4+4+3)
+    (3, 11, True, True, 4),
+    (2, 9, False, True, 4),    # per-step inner launches
+    (3, 8, True, False, 4),    # edges not first
+    (2, 9, True, True, 8),     # deeper zone: pairs over 2 ghost planes
+    (1, 7, True, True, 4),     # single rank, self-exchange
+])
+def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, shape, steps, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, fuse2, edge_first, gpad, q))
+             for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    ghosts, got = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    assert np.array_equal(got, _monolithic(shape, steps))
+    assert len(set(ghosts)) == 1, f"ranks picked different ghost depths {ghosts}"
+    ref = _monolithic(steps)
+    assert not np.isnan(got).any()
+    assert np.array_equal(got, ref), f"max diff {np.nanmax(np.abs(got - ref))}"
+
+
+def test_block_plan_shapes():
+    """The schedule's ranges: core/rim, shrinking pairs, edges first."""
+    from stochquant_amd.decomp import block_plan
+    ops = block_plan(64, 16, 16)
+    assert [o["op"] for o in ops[:4]] == ["exchange", "step", "wait_exchange", "step"]
+    assert (ops[1]["lo"], ops[1]["hi"]) == (1, 63)
+    assert (ops[3]["lo"], ops[3]["hi"], ops[3]["lo2"], ops[3]["hi2"]) == (-15, 1, 63, 79)
+    pairs = [o for o in ops if o["op"] == "pair"]
+    assert [(o["step"], o["lo"], o["hi"]) for o in pairs] == [(s, -(14 - s), 64 + 14 - s) for s in range(1, 15, 2)]
+    tail = [o for o in ops if o["step"] == 15]
+    assert [(o["op"], o["lo"], o["hi"]) for o in tail] == [("step", 0, 16), ("step", 48, 64), ("edges_done", 0, 0),
+                                                           ("step", 16, 48)]
+    # every step 1..g-1 covered exactly once, the last one ghost-free
+    ops = block_plan(12, 4, 3, fuse2=False, edge_first=False)
+    steps = [(o["step"], o["lo"], o["hi"]) for o in ops if o["op"] == "step"]
+    assert steps == [(0, 1, 11), (0, -2, 1), (1, -1, 13), (2, 0, 12)]
+    assert ops[-1]["op"] == "edges_done"
 
 
 def test_slab_bounds_cover_lattice():
