@@ -1,18 +1,20 @@
 #!/bin/bash
-# Run GPU steps in order; each under its own time limit.  A step that exits 0
-# or 1 (test failures) lets the next one run; anything else (fault, abort,
-# segfault, timeout) stops the script there.
-#   scripts/gpu_steps.sh NAME:SECONDS:"command" ...
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+# Run GPU steps in order, each under its own time limit; stop at the first
+# step that times out, aborts, segfaults or is killed (no further GPU step
+# after those), continue past ordinary failures.  Usage:
+#   bash scripts/gpu_steps.sh SECONDS 'cmd1' SECONDS 'cmd2' ...
 mkdir -p gpurun_out
 rc_all=0
-for spec in "$@"; do
-  name="${spec%%:*}"; rest="${spec#*:}"; secs="${rest%%:*}"; cmd="${rest#*:}"
-  echo "=== $name ($secs s): $cmd"
-  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.log" 2>&1
-  rc=$?
-  echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
-  [ $rc -ne 0 ] && rc_all=$rc
+while [ $# -ge 2 ]; do
+    t=$1; cmd=$2; shift 2
+    echo "=== [$t s] $cmd"
+    timeout -k 10 "$t" bash -c "$cmd"
+    rc=$?
+    echo "=== rc=$rc"
+    case $rc in
+        124|137|134|139|143) echo "=== stopping: GPU step ended abnormally"; exit $rc ;;
+        0) ;;
+        *) rc_all=$rc ;;
+    esac
 done
 exit $rc_all

@@ -266,9 +266,9 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo
     sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
     // planes per block: pinned, or as many as make one round of tb_blocks
     // blocks (a ragged second round costs more than the deeper chunks)
-    const int nyg = c->Ly / 8, span = zhi - zlo;
+    const int nyg = c->Ly / 8, nxseg = c->Lx / 256, span = zhi - zlo;
     // (the slabs of a loopback decomposition run concurrently on their own streams)
-    const int nzc_t = std::max(1, c->tb_blocks / (nyg * (int)c->slabs.size()));
+    const int nzc_t = std::max(1, c->tb_blocks / (nyg * nxseg * (int)c->slabs.size()));
     const int zb = c->tbz_pin ? c->tbz : std::max(1, (span + nzc_t - 1) / nzc_t);
     a.zlo = zlo;
     a.zhi = zhi;
@@ -276,9 +276,9 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo
     a.zc = zb;
     a.nzc = (span + zb - 1) / zb;
     a.periodic = periodic;
-    a.nxseg = 1;
+    a.nxseg = nxseg;
     a.nyg = nyg;
-    a.nunits = a.nyg * a.nzc;
+    a.nunits = a.nxseg * a.nyg * a.nzc;
     EvPair *e = nullptr;
     if (timed && c->profiling == 1) {
         int rc = ev_take(c, &e);
@@ -688,8 +688,12 @@ int create_phi4(sq_ctx *c) {
     // launches ran slower fused (29.1 vs 25.4 us per step, 2 slabs of 128
     // planes), while one RCCL slab of 256 planes gains (24.2 vs 26.0,
     // profiles/r01/fuse2_slabs.log).
+    // Rows of several 256-site segments fuse through the x-halo wave: measured
+    // (profiles/r02/sweep_tb2_*.log, us per step, fused vs one step per launch)
+    // 1024 x 1024 x 128 194 vs 225, 1024^3 1537 vs 1678, 512^3 197 vs 199 --
+    // a tie at 512-wide rows, which keep the per-step kernel.
     const char *fe = getenv("SQ_FUSE2");
-    const bool fuse = fe ? atoi(fe) != 0 : p.comm != SQ_COMM_LOOPBACK;
+    const bool fuse = fe ? atoi(fe) != 0 : (p.comm != SQ_COMM_LOOPBACK && c->Lx != 512);
     if (fuse && sq::phi4_tb2_supported(c->Lx, c->Ly) && (p.comm != SQ_COMM_NONE || c->slabs[0].nz >= 2)) {
         c->tbz = 16;
         if (const char *z = getenv("SQ_FUSE2_Z")) {
@@ -698,7 +702,9 @@ int create_phi4(sq_ctx *c) {
         }
         int ncu = 0;
         SQ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->dev));
-        c->tb_blocks = 2 * std::max(1, ncu);  // 68 VGPRs, 10 waves: two blocks per CU
+        // two blocks per CU (256-wide rows: 65 VGPRs, 10 waves; wider rows: 11 waves at <= 80)
+        c->tb_blocks = 2 * std::max(1, ncu);
+        if (const char *e = getenv("SQ_TB2_BLOCKS_PER_CU")) c->tb_blocks = std::max(1, atoi(e)) * std::max(1, ncu);
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;

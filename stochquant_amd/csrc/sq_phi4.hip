@@ -370,25 +370,37 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
 }
 
 // ----------------------------------------------------- two-step fusion ----
-// Steps s and s+1 in one pass over the field (temporal blocking), for
-// 256-wide rows: a single periodic slab, or the planes [zlo, zhi) of a slab
-// whose input is valid on [zlo-2, zhi+2) (deep-halo blocks).  A block of kTbWaves = 10 waves
-// owns kTbRows = 8 output rows [y0, y0+8) of a z-chunk [z0, z1); wave w
-// holds row y0-1+w.  Marching p over [z0-1, z1]:
-//   1. every wave loads input plane p+1 (its row and both y-halo rows) and
-//      updates its row of plane p by step s -> T(p) (the same site update,
-//      noise keyed by step s), keeps T in a 3-plane register queue and
-//      publishes it in LDS slot p % 3;
-//   2. barrier;
-//   3. waves 1..8 update their row of plane p-1 by step s+1 from T(p-2),
-//      T(p-1), T(p) (registers) and the y-neighbour rows of T(p-1) (LDS).
-// Rows y0-1, y0+8 and planes z0-1, z1 of T are recomputed by the adjacent
-// blocks too: the counter-based noise makes them bit-identical, so the
-// result equals two single steps bit for bit.  HBM traffic: one read and one
-// write of the field per two steps.  Three LDS slots: a slot is rewritten
-// two barriers after its last reader passed the barrier before its read.
+// Steps s and s+1 in one pass over the field (temporal blocking), for rows of
+// Lx = 256 S sites: a single periodic slab, or the planes [zlo, zhi) of a slab
+// whose input is valid on [zlo-2, zhi+2) (deep-halo blocks).  A block owns one
+// 256-site x-segment [x0, x0+256) of kTbRows = 8 output rows [y0, y0+8) of a
+// z-chunk [z0, z1).  Row wave w = 0..9 holds row y0-1+w of the segment (lane
+// l: sites x0+4l..x0+4l+3).  Marching p over [z0-1, z1]:
+//   1. every row wave loads input plane p+1 (its row and both y-halo rows),
+//      and, when S > 1, plane p's two sites just outside the segment (lane 0
+//      x0-1, lane 63 x0+256), and updates its row of plane p by step s ->
+//      T(p) (the same site update, noise keyed by step s); T stays in a
+//      3-plane register queue and is published in LDS slot p % 3;
+//   2. S > 1: the x-halo wave (w = 10) updates the 16 sites (x0-1 | x0+256,
+//      y0..y0+7) of plane p by step s from its own 5-point loads and publishes
+//      them in LDS -- the x-neighbours of the segment's edge lanes in step s+1;
+//   3. barrier;
+//   4. row waves 1..8 update their row of plane p-1 by step s+1 from T(p-2),
+//      T(p-1), T(p) (registers), the y-neighbour rows of T(p-1) (LDS) and, at
+//      the segment edges, the x-halo sites (LDS; S = 1: the DPP rotation wraps
+//      the periodic row), and store it with sc0 sc1.
+// Rows y0-1, y0+8, planes z0-1, z1 and the x-halo sites of T are recomputed
+// by the blocks that own them too: the counter-based noise makes them
+// bit-identical, so the result equals two single steps bit for bit.  HBM
+// traffic: one read and one write of the field per two steps.  Three LDS
+// slots: a slot is rewritten two barriers after its last reader passed the
+// barrier before its read.
+// Measured and not adopted (profiles/r02/): loads two planes ahead with the
+// z-1 neighbour read from a fourth LDS slot (90 VGPRs at S = 1, 109 at S > 1):
+// 256^3 21.4 -> 21.8 us per step, 512^3 197 -> 330 us -- the kernel is not
+// waiting on its loads.
 constexpr int kTbRows = 8;
-constexpr int kTbWaves = kTbRows + 2;
+constexpr int kTbWaves = kTbRows + 2;  // row waves; S > 1 adds the x-halo wave
 
 // Padded plane of local plane zl: the periodic slab wraps (|overflow| <= 2),
 // a slab of a decomposition reads its ghost zone.
@@ -413,102 +425,184 @@ __device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, int zl, uint32
     return xi;
 }
 
+// One plane of a row wave's inputs: its row and the row's two y-neighbours.
+// The x-halo wave keeps the centre values of its sites in row.x, so the two
+// roles share one register queue.
 struct TbIn {
-    float4 row, hm, hp;  // the wave's row and its two y-neighbours at one plane
+    float4 row, hm, hp;
 };
 
-// One plane of the march: see above.  I0 (p-1), I1 (p), I2 (p+1, loaded here);
-// T0 (p-2), T1 (p-1), T2 (p, computed here).
-template <bool NZ>
-__device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, int p, int z0, const TbIn &I0, const TbIn &I1,
-                                         TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
-                                         float4 (*lds)[kTbWaves][64], int w, int lane, bool outw,
-                                         uint32_t voff, uint32_t vm, uint32_t vp, uint32_t qoff, size_t plane,
-                                         uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi,
-                                         uint32_t slo1, uint32_t shi1, int &bad) {
-    {
-        const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, tb_pidx(A, p + 1), plane, pbytes);
-        I2.row = bload4(rs, voff);
-        I2.hm = bload4(rs, vm);
-        I2.hp = bload4(rs, vp);
+// Per-block constants of the march.
+struct TbCtx {
+    size_t plane;
+    uint32_t pbytes, qplane;
+    // byte offsets in a plane and the Philox quad offset.  Row waves: voff
+    // their row, vm / vp its y-neighbours, vex the site just outside the
+    // segment (lane 0 left, lane 63 right).  x-halo wave lanes (sharing the
+    // registers): voff the site, vm / vp its y-neighbours, vex / vx2 its x-1 / x+1.
+    uint32_t voff, vm, vp, vex, vx2, qoff;
+    uint32_t slo, shi, slo1, shi1;
+    int z0, w, lane;
+    bool outw;
+};
+
+__device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym, float yp, float zm, float zp,
+                                         float xi, const Phi4StepArgs &A, bool nz) {
+    const float nb = ((xm + xp) + (ym + yp)) + (zm + zp);
+    const float lap = __builtin_fmaf(-6.0f, phi, nb);
+    const float g = __builtin_fmaf(A.lam6, phi * phi, A.m2);
+    const float drift = __builtin_fmaf(-phi, g, lap);
+    const float det = __builtin_fmaf(A.h, drift, phi);
+    const float v = nz ? __builtin_fmaf(A.sig, xi, det) : det;
+    return fmaxf(fminf(v, A.clampv), -A.clampv);
+}
+
+// One plane of the march.  Row waves: I0 (p-1), I1 (p), I2 (p+1, loaded
+// here); T0 (p-2), T1 (p-1), T2 (p, computed here).  The x-halo wave: the
+// centres of its sites at the same planes in row.x.
+template <bool NZ, bool WIDE>
+__device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, int p, const TbIn &I0,
+                                         const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
+                                         float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], int &bad) {
+    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, tb_pidx(A, p + 1), K.plane, K.pbytes);
+    // S > 1: plane p's values at the segment's outer x-neighbours (lane 0 x0-1,
+    // lane 63 x0+256) and at the x-halo sites' in-plane neighbours are loaded
+    // in the iteration that uses them, like plane p+1 itself
+    const __amdgpu_buffer_rsrc_t rc = plane_rsrc(A.in, tb_pidx(A, p), K.plane, K.pbytes);
+    if (!WIDE || K.w < kTbWaves) {
+        I2.row = bload4(rs, K.voff);
+        I2.hm = bload4(rs, K.vm);
+        I2.hp = bload4(rs, K.vp);
+        float ex = 0.f;
+        if constexpr (WIDE) ex = bload1(rc, K.vex);
+        const f32x4n xa = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
+        float lft = from_left_lane(I1.row.w), rgt = from_right_lane(I1.row.x);
+        if constexpr (WIDE) {
+            if (K.lane == 0) lft = ex;
+            if (K.lane == 63) rgt = ex;
+        }
+        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A);
+        if (A.flag != nullptr) {
+            const float m = fmaxf(fmaxf(fabsf(T2.x), fabsf(T2.y)), fmaxf(fabsf(T2.z), fabsf(T2.w)));
+            bad |= (int)(m >= A.clampv);
+        }
+        const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
+        lds[sl][K.w][K.lane] = T2;
+    } else {
+        // the x-halo wave: step s at its 16 sites of plane p
+        I2.row.x = bload1(rs, K.voff);
+        const float xm = bload1(rc, K.vex), xp = bload1(rc, K.vx2), ym = bload1(rc, K.vm), yp = bload1(rc, K.vp);
+        const f32x4n n = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
+        // lanes 0..7 hold x0-1 (component 3 of its quad), 8..15 x0+256 (component 0)
+        const float xi = K.lane >= 8 ? n.a : n.d;
+        const float t = tb_site(I1.row.x, xm, xp, ym, yp, I0.row.x, I2.row.x, xi, A, NZ);
+        if (K.lane < 16) tx[(p % 3 + 3) % 3][(K.lane & 7) + 1][K.lane >> 3] = t;
     }
-    const f32x4n xa = tb_noise<NZ>(A, p, qoff, qplane, slo, shi);
-    f32x4n xb = f32x4n{0.f, 0.f, 0.f, 0.f};
-    const bool doB = outw && p > z0;
-    if (doB) xb = tb_noise<NZ>(A, p - 1, qoff, qplane, slo1, shi1);
-    T2 = site_update4<NZ>(I1.row, from_left_lane(I1.row.w), from_right_lane(I1.row.x), I1.hm, I1.hp, I0.row,
-                          I2.row, xa, A);
-    if (A.flag != nullptr) {
-        const float m = fmaxf(fmaxf(fabsf(T2.x), fabsf(T2.y)), fmaxf(fabsf(T2.z), fabsf(T2.w)));
-        bad |= (int)(m >= A.clampv);
-    }
-    const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
-    lds[sl][w][lane] = T2;
     __syncthreads();
-    if (doB) {
+    if (K.outw && p > K.z0) {
+        const f32x4n xb = tb_noise<NZ>(A, p - 1, K.qoff, K.qplane, K.slo1, K.shi1);
         const int sp = ((p + 2) % 3 + 3) % 3;  // slot of plane p-1
-        const float4 up = lds[sp][w - 1][lane], dn = lds[sp][w + 1][lane];
-        const float4 o = site_update4<NZ>(T1, from_left_lane(T1.w), from_right_lane(T1.x), up, dn, T0, T2, xb, A);
+        const float4 up = lds[sp][K.w - 1][K.lane], dn = lds[sp][K.w + 1][K.lane];
+        float lft = from_left_lane(T1.w), rgt = from_right_lane(T1.x);
+        if constexpr (WIDE) {
+            if (K.lane == 0) lft = tx[sp][K.w][0];
+            if (K.lane == 63) rgt = tx[sp][K.w][1];
+        }
+        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A);
         if (A.flag != nullptr) {
             const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
             bad |= (int)(m >= A.clampv);
         }
-        const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, plane, pbytes);
-        bstore4<17>(ws, voff, o);
+        const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
+        bstore4<17>(ws, K.voff, o);
     }
 }
 
-// 68 VGPRs: two 10-wave blocks per CU.  A 64-VGPR budget (three blocks per
-// CU) measured slower at every z-chunk (profiles/r01/fuse2_sweep.log): the
-// kernel is issue-bound, not latency-bound.
-template <bool NZ>
-__global__ __launch_bounds__(kTbWaves * 64) void phi4_tb2_kernel(const Phi4StepArgs A) {
+// WPE: waves per SIMD the registers are budgeted for (S > 1: 6 = two 11-wave
+// blocks per CU at <= 80 VGPRs, spilling 9; 1 = unconstrained, 85 VGPRs).
+// 256-wide rows: 65 VGPRs, two 10-wave blocks per CU.  A 64-VGPR budget
+// (three blocks per CU) measured slower at every z-chunk
+// (profiles/r01/fuse2_sweep.log).
+template <bool NZ, bool WIDE, int WPE>
+__global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
+__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A) {
     const int nb = gridDim.x, b = blockIdx.x;
-    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // y-bands of a z-chunk on one XCD
-    const int yb = lb % A.nyg, zk = lb / A.nyg;
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
+    // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
+    // one XCD: the blocks sharing halo rows, edge columns and chunk-edge planes
+    // meet in that XCD's L2
+    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
+    const int yb = lb % A.nyg, rest = lb / A.nyg;
+    const int xs = WIDE ? rest % A.nxseg : 0, zk = WIDE ? rest / A.nxseg : rest;
     const int Lx = A.Lx, Ly = A.Ly;
-    int y = yb * kTbRows - 1 + w;
-    y = y < 0 ? y + Ly : (y >= Ly ? y - Ly : y);
-    const int ym = y == 0 ? Ly - 1 : y - 1, yp = y == Ly - 1 ? 0 : y + 1;
-    const uint32_t voff = (uint32_t)((y * Lx + 4 * lane) * 4);
-    const uint32_t vm = (uint32_t)((ym * Lx + 4 * lane) * 4), vp = (uint32_t)((yp * Lx + 4 * lane) * 4);
-    const uint32_t qoff = (uint32_t)((y * Lx + 4 * lane) >> 2);
-    const bool outw = w >= 1 && w <= kTbRows;
-    const int z0 = A.zlo + zk * A.zc, z1 = min(z0 + A.zc, A.zhi);
-    const size_t plane = (size_t)Lx * (size_t)Ly;
-    const uint32_t pbytes = (uint32_t)(plane * sizeof(float));
-    const uint32_t qplane = (uint32_t)(plane >> 2);
+    const int x0 = 256 * xs;
+    TbCtx K;
+    K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    K.lane = threadIdx.x & 63;
+    K.outw = K.w >= 1 && K.w <= kTbRows;
+    K.z0 = A.zlo + zk * A.zc;
+    const int z1 = min(K.z0 + A.zc, A.zhi);
+    K.plane = (size_t)Lx * (size_t)Ly;
+    K.pbytes = (uint32_t)(K.plane * sizeof(float));
+    K.qplane = (uint32_t)(K.plane >> 2);
     const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
-    const uint32_t slo = (uint32_t)s0, shi = (uint32_t)(s0 >> 32), slo1 = (uint32_t)s1, shi1 = (uint32_t)(s1 >> 32);
+    K.slo = (uint32_t)s0;
+    K.shi = (uint32_t)(s0 >> 32);
+    K.slo1 = (uint32_t)s1;
+    K.shi1 = (uint32_t)(s1 >> 32);
+    const int xl = (x0 == 0 ? Lx : x0) - 1, xr = x0 + 256 == Lx ? 0 : x0 + 256;  // just outside the segment
+    auto wrapy = [Ly](int y) { return y < 0 ? y + Ly : (y >= Ly ? y - Ly : y); };
+    if (!WIDE || K.w < kTbWaves) {
+        const int y = wrapy(yb * kTbRows - 1 + K.w);
+        const int ym = wrapy(y - 1), yp = wrapy(y + 1);
+        K.voff = (uint32_t)((y * Lx + x0 + 4 * K.lane) * 4);
+        K.vm = (uint32_t)((ym * Lx + x0 + 4 * K.lane) * 4);
+        K.vp = (uint32_t)((yp * Lx + x0 + 4 * K.lane) * 4);
+        K.vex = (uint32_t)((y * Lx + (K.lane == 63 ? xr : xl)) * 4);
+        K.vx2 = 0;
+        K.qoff = (uint32_t)((y * Lx + x0 + 4 * K.lane) >> 2);
+    } else {  // x-halo wave lanes 0..7: (x0-1, y0+l); 8..15: (x0+256, y0+l-8); the rest repeat lane 0
+        const int l = K.lane < 16 ? K.lane : 0;
+        const int y = wrapy(yb * kTbRows + (l & 7)), ym = wrapy(y - 1), yp = wrapy(y + 1);
+        const int xe = (l >> 3) ? xr : xl;
+        const int xem = xe == 0 ? Lx - 1 : xe - 1, xep = xe == Lx - 1 ? 0 : xe + 1;
+        K.voff = (uint32_t)((y * Lx + xe) * 4);
+        K.vex = (uint32_t)((y * Lx + xem) * 4);
+        K.vx2 = (uint32_t)((y * Lx + xep) * 4);
+        K.vm = (uint32_t)((ym * Lx + xe) * 4);
+        K.vp = (uint32_t)((yp * Lx + xe) * 4);
+        K.qoff = (uint32_t)((y * Lx + xe) >> 2);
+    }
     __shared__ float4 lds[3][kTbWaves][64];
+    __shared__ float tx[WIDE ? 3 : 1][kTbWaves][2];
 
     TbIn I0, I1, I2;
     {
-        const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, z0 - 2), plane, pbytes);
-        I0.row = bload4(r0, voff);
-        I0.hm = I0.hp = I0.row;
-        const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(A.in, tb_pidx(A, z0 - 1), plane, pbytes);
-        I1.row = bload4(r1, voff);
-        I1.hm = bload4(r1, vm);
-        I1.hp = bload4(r1, vp);
+        const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
+        const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 1), K.plane, K.pbytes);
+        if (!WIDE || K.w < kTbWaves) {
+            I0.row = bload4(r0, K.voff);
+            I0.hm = I0.hp = I0.row;
+            I1.row = bload4(r1, K.voff);
+            I1.hm = bload4(r1, K.vm);
+            I1.hp = bload4(r1, K.vp);
+        } else {
+            I0.row = make_float4(bload1(r0, K.voff), 0.f, 0.f, 0.f);
+            I1.row = make_float4(bload1(r1, K.voff), 0.f, 0.f, 0.f);
+            I0.hm = I0.hp = I1.hm = I1.hp = I0.row;
+        }
     }
     float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
     int bad = 0;
     // three-plane queues unrolled three ways so no rotation moves are emitted
-    for (int p = z0 - 1; p <= z1; p += 3) {
-        tb_plane<NZ>(A, p, z0, I0, I1, I2, T0, T1, T2, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
-                     qplane, slo, shi, slo1, shi1, bad);
+    for (int p = K.z0 - 1; p <= z1; p += 3) {
+        tb_plane<NZ, WIDE>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, bad);
         if (p + 1 > z1) break;
-        tb_plane<NZ>(A, p + 1, z0, I1, I2, I0, T1, T2, T0, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
-                     qplane, slo, shi, slo1, shi1, bad);
+        tb_plane<NZ, WIDE>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, bad);
         if (p + 2 > z1) break;
-        tb_plane<NZ>(A, p + 2, z0, I2, I0, I1, T2, T0, T1, lds, w, lane, outw, voff, vm, vp, qoff, plane, pbytes,
-                     qplane, slo, shi, slo1, shi1, bad);
+        tb_plane<NZ, WIDE>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, bad);
     }
     if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && lane == 0) atomicOr(A.flag, 1);
+        if (__ballot(bad) != 0ull && K.lane == 0) atomicOr(A.flag, 1);
     }
 }
 
@@ -691,15 +785,26 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
     }
 }
 
-bool phi4_tb2_supported(int Lx, int Ly) { return Lx == 256 && Ly % kTbRows == 0; }
+bool phi4_tb2_supported(int Lx, int Ly) { return Lx % 256 == 0 && Ly % kTbRows == 0; }
 
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0) return hipErrorInvalidValue;
+    if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0 || a.nxseg != a.Lx / 256 || a.nyg != a.Ly / kTbRows ||
+        a.nunits != a.nxseg * a.nyg * a.nzc || (long long)a.zc * a.nzc < (long long)(a.zhi - a.zlo))
+        return hipErrorInvalidValue;
     if (a.periodic ? (a.nz < 2 || a.zlo != 0 || a.zhi != a.nz)
                    : (a.zlo - 2 < -a.gz || a.zhi + 2 > a.nz + a.gz))  // input planes outside the buffer
         return hipErrorInvalidValue;
-    const dim3 grid((unsigned)a.nunits), block(kTbWaves * 64);
-    const void *fn = a.sig != 0.0f ? (const void *)&phi4_tb2_kernel<true> : (const void *)&phi4_tb2_kernel<false>;
+    const bool wide = a.nxseg > 1;
+    const dim3 grid((unsigned)a.nunits), block((kTbWaves + (wide ? 1 : 0)) * 64);
+    const bool nz = a.sig != 0.0f;
+    static const int wpe = getenv("SQ_TB2_WPE") ? atoi(getenv("SQ_TB2_WPE")) : 6;
+    const void *fn;
+    if (wide && wpe == 6)
+        fn = nz ? (const void *)&phi4_tb2_kernel<true, true, 6> : (const void *)&phi4_tb2_kernel<false, true, 6>;
+    else if (wide)
+        fn = nz ? (const void *)&phi4_tb2_kernel<true, true, 1> : (const void *)&phi4_tb2_kernel<false, true, 1>;
+    else
+        fn = nz ? (const void *)&phi4_tb2_kernel<true, false, 1> : (const void *)&phi4_tb2_kernel<false, false, 1>;
     Phi4StepArgs q = a;
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
