@@ -174,6 +174,19 @@ int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
 int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
                        int *nops);
 int sq_phi4_pick_ghost(const double *ms, int n);
+/* PHI4 frame stability (the heuristic of tau_kernel.cl:135-143 restated for
+ * the 3-D lattice).  Every frame records per step j the maximum
+ * M_j of phi', the drift increment D_j = |phi' - phi - sigma xi| at the sites
+ * attaining it (the largest on ties) and A_j = max |phi'|, reduced over all
+ * slabs and ranks (RCCL max); the frame is unstable -- rolled back like a
+ * clamp / NaN hit -- at the first step with M_j > T and D_j > V, where T is
+ * the previous step's maximum and V the running max |phi| of the steps before
+ * (carried across frames and never rolled back, as lrgEl / lrgVl; initialised
+ * from the field at the first frame).  sq_phi4_stability returns {T, V}, the
+ * step at which the last frame fired (-1: none) and that frame's records
+ * (n <= loops); sq_phi4_set_stability sets T and V. */
+int sq_phi4_stability(sq_ctx *ctx, double state[2], int *fired_step, float *M, float *D, float *A, int n);
+int sq_phi4_set_stability(sq_ctx *ctx, double T, double V);
 /* PHI4 observables over this process' slab: out[0] = sum phi, out[1] = sum
  * phi^2, out[2] = max |phi| (double accumulation on device). */
 int sq_moments(sq_ctx *ctx, double out[3]);

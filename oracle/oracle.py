@@ -81,6 +81,9 @@ def lib():
         L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_uint64]
         L.orc_phi4_init.argtypes = [ctypes.POINTER(Phi4), ctypes.c_float, _F]
+        L.orc_phi4_step_stab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_uint64, _F]
+        L.orc_phi4_stab_rule.restype = ctypes.c_int
+        L.orc_phi4_stab_rule.argtypes = [_F, _F, _F, _F, _F, ctypes.c_int]
         L.orc_phi4_step_range.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]
         L.orc_phi4_sigma.restype = ctypes.c_float
@@ -214,6 +217,25 @@ def phi4_step_range(p, src, dst, gpad, lo, hi, z0, step):
     assert -gpad < lo and hi < nz + gpad, "the range needs one readable plane on either side"
     lib().orc_phi4_step_range(ctypes.byref(p), src.ctypes.data_as(_F), dst.ctypes.data_as(_F), nz, gpad, lo, hi,
                               z0, step)
+
+
+def phi4_frame_stab(p, phi, steps, step0, T, V):
+    """`steps` steps from phi with the per-step stability records and the
+    frame rule: returns (phi', M, D, A, fired, T', V')."""
+    phi = np.ascontiguousarray(phi, dtype=np.float32)
+    M, D, A = (np.zeros(steps, np.float32) for _ in range(3))
+    rec = np.zeros(3, np.float32)
+    for j in range(steps):
+        out = np.empty_like(phi)
+        lib().orc_phi4_step_stab(ctypes.byref(p), phi.ctypes.data_as(_F), out.ctypes.data_as(_F), step0 + j,
+                                 rec.ctypes.data_as(_F))
+        M[j], D[j], A[j] = rec
+        phi = out
+    t = np.array([T], np.float32)
+    v = np.array([V], np.float32)
+    fired = lib().orc_phi4_stab_rule(t.ctypes.data_as(_F), v.ctypes.data_as(_F), M.ctypes.data_as(_F),
+                                     D.ctypes.data_as(_F), A.ctypes.data_as(_F), steps)
+    return phi, M, D, A, fired, float(t[0]), float(v[0])
 
 
 def phi4_init(p, amp):

@@ -23,6 +23,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 #include "sq_oracle.h"
 #ifdef _OPENMP
 #include <omp.h>
@@ -31,10 +32,32 @@
 float orc_phi4_sigma(float h, double C) { return (float)(sqrt(2.0 * (double)h) * C); }
 float orc_phi4_lam6(float lam) { return (float)((double)lam / 6.0); }
 
+/* Order-preserving float -> uint32 map (larger float, larger code). */
+static uint32_t ord_f32(float v)
+{
+    uint32_t u;
+    memcpy(&u, &v, 4);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+/* The stability record of one site: key = ord(phi') << 32 |
+ * bits(|phi' - phi - sigma xi|), so the maximum key over a step is its maximum
+ * phi' with the largest drift increment among the sites attaining it. */
+static void stab_site(uint64_t *key, float *amax, float o, float c, float xi, float sig)
+{
+    const float dn = fabsf(fmaf(-sig, xi, o - c));
+    uint32_t db;
+    memcpy(&db, &dn, 4);
+    const uint64_t k = ((uint64_t)ord_f32(o) << 32) | db;
+    if (k > *key) *key = k;
+    if (fabsf(o) > *amax) *amax = fabsf(o);
+}
+
 /* One plane of the update: c = plane z, zm/zp = planes z-1, z+1 (already
- * resolved by the caller: periodic wrap or ghost planes), zg = global z. */
+ * resolved by the caller: periodic wrap or ghost planes), zg = global z.
+ * key / amax (nullable): the step's stability record, accumulated. */
 static void phi4_plane(const orc_phi4 *p, const float *cz, const float *czmp, const float *czpp,
-                       float *oz, uint64_t zg, uint64_t step)
+                       float *oz, uint64_t zg, uint64_t step, uint64_t *key, float *amax)
 {
     const int Lx = p->Lx, Ly = p->Ly;
     const float h = p->h, m2 = p->m2, lam6 = orc_phi4_lam6(p->lam);
@@ -62,6 +85,7 @@ static void phi4_plane(const orc_phi4 *p, const float *cz, const float *czmp, co
                 float v = fmaf(sig, xi[k], fmaf(h, drift, phi));
                 v = isnan(v) ? mx : (v > mx ? mx : (v < -mx ? -mx : v));
                 o[x] = v;
+                if (key) stab_site(key, amax, v, phi, xi[k], sig);
             }
         }
     }
@@ -78,8 +102,37 @@ void orc_phi4_step(const orc_phi4 *p, const float *in, float *out, uint64_t step
     for (int z = 0; z < Lz; ++z) {
         const int zm = (z + Lz - 1) % Lz, zp = (z + 1) % Lz;
         phi4_plane(p, in + (size_t)z * plane, in + (size_t)zm * plane, in + (size_t)zp * plane,
-                   out + (size_t)z * plane, (uint64_t)z, step);
+                   out + (size_t)z * plane, (uint64_t)z, step, NULL, NULL);
     }
+}
+
+void orc_phi4_step_stab(const orc_phi4 *p, const float *in, float *out, uint64_t step, float rec[3])
+{
+    const int Lz = p->Lz;
+    const size_t plane = (size_t)p->Lx * p->Ly;
+    uint64_t key = 0;
+    float amax = 0.f;
+    for (int z = 0; z < Lz; ++z) {
+        const int zm = (z + Lz - 1) % Lz, zp = (z + 1) % Lz;
+        phi4_plane(p, in + (size_t)z * plane, in + (size_t)zm * plane, in + (size_t)zp * plane,
+                   out + (size_t)z * plane, (uint64_t)z, step, &key, &amax);
+    }
+    const uint32_t o = (uint32_t)(key >> 32), db = (uint32_t)key;
+    const uint32_t u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    memcpy(&rec[0], &u, 4);
+    memcpy(&rec[1], &db, 4);
+    rec[2] = amax;
+}
+
+int orc_phi4_stab_rule(float *T, float *V, const float *M, const float *D, const float *A, int n)
+{
+    for (int j = 0; j < n; ++j) {
+        const int fired = M[j] > *T && D[j] > *V;
+        *T = M[j];
+        if (A[j] > *V) *V = A[j];
+        if (fired) return j;
+    }
+    return -1;
 }
 
 /* Slab form used by the decomposition tests: `in` holds nz+2 planes (ghost,
@@ -90,7 +143,7 @@ void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, 
     const size_t plane = (size_t)p->Lx * p->Ly;
     for (int z = 0; z < nz; ++z)
         phi4_plane(p, in + (size_t)(z + 1) * plane, in + (size_t)z * plane, in + (size_t)(z + 2) * plane,
-                   out + (size_t)z * plane, z0 + (uint64_t)z, step);
+                   out + (size_t)z * plane, z0 + (uint64_t)z, step, NULL, NULL);
 }
 
 void orc_phi4_step_range(const orc_phi4 *p, const float *in, float *out, int nz, int gpad, int lo, int hi,
@@ -103,7 +156,7 @@ void orc_phi4_step_range(const orc_phi4 *p, const float *in, float *out, int nz,
         const int64_t zg = (((int64_t)z0 + zl) % Lz + Lz) % Lz;
         const size_t c = (size_t)(zl + gpad);
         phi4_plane(p, in + c * plane, in + (c - 1) * plane, in + (c + 1) * plane, out + c * plane,
-                   (uint64_t)zg, step);
+                   (uint64_t)zg, step, NULL, NULL);
     }
 }
 

@@ -112,6 +112,14 @@ void orc_phi4_step_slab(const orc_phi4 *p, const float *in, float *out, int nz, 
  * plane zl = (z0 + zl) mod Lz (ghost-zone planes wrap). */
 void orc_phi4_step_range(const orc_phi4 *p, const float *in, float *out, int nz, int gpad, int lo, int hi,
                          uint64_t z0, uint64_t step);
+/* One step with the stability record of DESIGN.md §7 (the 3-D restatement of
+ * tau_kernel.cl:135-143): rec = {M = max phi', D = max over the sites
+ * attaining M of |phi' - phi - sigma xi| (fp32, fmaf(-sigma, xi, phi' - phi)),
+ * A = max |phi'|}.  Single-threaded. */
+void orc_phi4_step_stab(const orc_phi4 *p, const float *in, float *out, uint64_t step, float rec[3]);
+/* The frame rule over n step records: returns the first step with M > T and
+ * D > V (-1: none); T <- M_j and V <- max(V, A_j) through that step. */
+int orc_phi4_stab_rule(float *T, float *V, const float *M, const float *D, const float *A, int n);
 /* Derived float parameters exactly as the product computes them. */
 float orc_phi4_sigma(float h, double C);
 float orc_phi4_lam6(float lam);

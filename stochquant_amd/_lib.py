@@ -111,6 +111,8 @@ SIGNATURES = {
     "sq_phi4_block_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
     "sq_phi4_pick_ghost": (ctypes.c_int, [_D, ctypes.c_int]),
+    "sq_phi4_stability": (ctypes.c_int, [_P, _D, _I, _F, _F, _F, ctypes.c_int]),
+    "sq_phi4_set_stability": (ctypes.c_int, [_P, ctypes.c_double, ctypes.c_double]),
     "sq_qm1d_set_ordering": (ctypes.c_int, [_P, ctypes.c_int]),
     "sq_qm1d_set_lcg_seed": (ctypes.c_int, [_P, ctypes.c_ulonglong]),
     "sq_qm1d_get_lcg_seed": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong)]),

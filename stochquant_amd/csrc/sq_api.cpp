@@ -73,6 +73,14 @@ struct EvPair {
     hipEvent_t a, b;
 };
 
+// Inverse of the kernels' order-preserving float -> uint map (sq_phi4.hip ord_f32).
+float unord_f32(unsigned int o) {
+    const unsigned int u = (o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o;
+    float f;
+    memcpy(&f, &u, sizeof f);
+    return f;
+}
+
 double host_intconst(int pot) {  // tau_kernel.cl:196-200,237-246 (float arithmetic)
     if (pot == 3)
         return (double)(sqrtf((float)3.) * powf((float)2., (float)(-5. / 4.)) *
@@ -131,7 +139,16 @@ struct sq_ctx {
     bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     double *dacc = nullptr;
-    unsigned int *dmax = nullptr;
+    unsigned int *dmax = nullptr;  // [0] max |phi| bits, [1] ordered max phi
+    // stability heuristic of phi4 frames (tau_kernel.cl:135-143):
+    // per-step device records of the current frame, kStabSlots words per step
+    unsigned long long *st_md = nullptr;
+    unsigned int *st_a = nullptr;
+    unsigned long long frame_step0 = 0;  // Philox step of the frame's first step
+    bool stab_init = false;              // T, V set from the field at the first frame
+    float stab_T = 0, stab_V = 0;        // carried across frames, never rolled back (as lrgEl / lrgVl)
+    int stab_fired = -1;                 // step of the last frame at which the rule fired, -1 none
+    std::vector<float> rec_M, rec_D, rec_A;  // the last frame's per-step records
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
@@ -221,6 +238,13 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.s_lo = (uint32_t)c->step;
     a.s_hi = (uint32_t)(c->step >> 32);
     a.flag = c->in_frame ? c->flag : nullptr;  // the guard flag only feeds a frame's rollback
+    a.st_md = nullptr;
+    a.st_a = nullptr;
+    if (c->in_frame && c->st_md != nullptr) {
+        const size_t k = (size_t)(c->step - c->frame_step0) * sq::kStabSlots;
+        a.st_md = c->st_md + k;
+        a.st_a = c->st_a + k;
+    }
     return a;
 }
 
@@ -655,7 +679,11 @@ int create_phi4(sq_ctx *c) {
     SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
     SQ_HIP(hipMemset(c->flag, 0, sizeof(int)));
     SQ_HIP(hipMalloc(&c->dacc, 2 * sizeof(double)));
-    SQ_HIP(hipMalloc(&c->dmax, sizeof(unsigned int)));
+    SQ_HIP(hipMalloc(&c->dmax, 2 * sizeof(unsigned int)));
+    if (p.loops >= 1) {
+        SQ_HIP(hipMalloc(&c->st_md, sizeof(unsigned long long) * sq::kStabSlots * (size_t)p.loops));
+        SQ_HIP(hipMalloc(&c->st_a, sizeof(unsigned int) * sq::kStabSlots * (size_t)p.loops));
+    }
     if (p.comm == SQ_COMM_RCCL) {
         ncclUniqueId id;
         static_assert(sizeof(id.internal) <= 128, "ncclUniqueId size");
@@ -925,10 +953,56 @@ void adapt(sq_ctx *c, int stable) {  // tauhost.c:523-529,537-541
     }
 }
 
+// max phi and max |phi| over the whole lattice (all slabs, all ranks).
+int phi4_field_max(sq_ctx *c, float *mx_phi, float *mx_abs) {
+    unsigned int m[2] = {0, 0};
+    for (auto &s : c->slabs) {
+        unsigned int t[2];
+        SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));
+        SQ_HIP(hipMemsetAsync(c->dmax, 0, 2 * sizeof(unsigned int), s.sA));
+        SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane_floats(c), c->dacc,
+                                       c->dmax, s.sA));
+        if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1)
+            SQ_NCCL(ncclAllReduce(c->dmax, c->dmax, 2, ncclUint32, ncclMax, c->comm, s.sA));
+        SQ_HIP(hipMemcpyAsync(t, c->dmax, sizeof t, hipMemcpyDeviceToHost, s.sA));
+        SQ_HIP(hipStreamSynchronize(s.sA));
+        m[0] = std::max(m[0], t[0]);
+        m[1] = std::max(m[1], t[1]);
+    }
+    memcpy(mx_abs, &m[0], sizeof(float));
+    *mx_phi = unord_f32(m[1]);
+    return SQ_OK;
+}
+
+// The stability heuristic of tau_kernel.cl:135-143, restated for the 3-D
+// lattice from per-step records: step j has a new leader when
+// its maximum M_j exceeds T (the maximum of the step before, carried across
+// frames); the frame is unstable at the first leader whose drift increment
+// D_j = |phi' - phi - sigma xi| at the maximum exceeds V, the running maximum
+// of |phi| of the steps before.  T and V are updated through that step (the
+// reference breaks after it) and never rolled back.
+int stab_rule(float &T, float &V, const float *M, const float *D, const float *A, int n) {
+    for (int j = 0; j < n; ++j) {
+        const bool fired = M[j] > T && D[j] > V;
+        T = M[j];
+        V = std::max(V, A[j]);
+        if (fired) return j;
+    }
+    return -1;
+}
+
 int phi4_frame(sq_ctx *c, int *stable) {
     const size_t plane = plane_floats(c);
     int rc = phi4_join(c);
     if (rc) return rc;
+    if (!c->stab_init) {  // the first frame's leader value and running max: the field itself
+        rc = phi4_field_max(c, &c->stab_T, &c->stab_V);
+        if (rc) return rc;
+        c->stab_init = true;
+    }
+    const size_t nrec = (size_t)sq::kStabSlots * (size_t)c->p.loops;
+    SQ_HIP(hipMemsetAsync(c->st_md, 0, sizeof(unsigned long long) * nrec, c->slabs[0].sA));
+    SQ_HIP(hipMemsetAsync(c->st_a, 0, sizeof(unsigned int) * nrec, c->slabs[0].sA));
     for (auto &s : c->slabs) {  // frame-start snapshot, kept on device
         const size_t bytes = (size_t)s.nz * plane * sizeof(float);
         if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
@@ -938,6 +1012,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     rc = phi4_join(c);
     if (rc) return rc;
     c->in_frame = true;
+    c->frame_step0 = c->step;
     rc = phi4_steps(c, c->p.loops);
     c->in_frame = false;
     if (rc) return rc;
@@ -945,12 +1020,37 @@ int phi4_frame(sq_ctx *c, int *stable) {
     if (rc) return rc;
     Slab &s0 = c->slabs[0];
     if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1) {
+        SQ_NCCL(ncclGroupStart());
         SQ_NCCL(ncclAllReduce(c->flag, c->flag, 1, ncclInt32, ncclMax, c->comm, s0.sA));
+        SQ_NCCL(ncclAllReduce(c->st_md, c->st_md, nrec, ncclUint64, ncclMax, c->comm, s0.sA));
+        SQ_NCCL(ncclAllReduce(c->st_a, c->st_a, nrec, ncclUint32, ncclMax, c->comm, s0.sA));
+        SQ_NCCL(ncclGroupEnd());
     }
     int h = 0;
+    std::vector<unsigned long long> md(nrec);
+    std::vector<unsigned int> am(nrec);
     SQ_HIP(hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, s0.sA));
+    SQ_HIP(hipMemcpyAsync(md.data(), c->st_md, sizeof(unsigned long long) * nrec, hipMemcpyDeviceToHost, s0.sA));
+    SQ_HIP(hipMemcpyAsync(am.data(), c->st_a, sizeof(unsigned int) * nrec, hipMemcpyDeviceToHost, s0.sA));
     SQ_HIP(hipStreamSynchronize(s0.sA));
-    *stable = h ? 0 : 1;
+    const int L = c->p.loops;
+    c->rec_M.assign(L, 0.f);
+    c->rec_D.assign(L, 0.f);
+    c->rec_A.assign(L, 0.f);
+    for (int j = 0; j < L; ++j) {
+        unsigned long long k = 0;
+        unsigned int a = 0;
+        for (int i = 0; i < sq::kStabSlots; ++i) {
+            k = std::max(k, md[(size_t)j * sq::kStabSlots + i]);
+            a = std::max(a, am[(size_t)j * sq::kStabSlots + i]);
+        }
+        c->rec_M[j] = unord_f32((unsigned int)(k >> 32));
+        const unsigned int db = (unsigned int)k;
+        memcpy(&c->rec_D[j], &db, sizeof(float));
+        memcpy(&c->rec_A[j], &a, sizeof(float));
+    }
+    c->stab_fired = stab_rule(c->stab_T, c->stab_V, c->rec_M.data(), c->rec_D.data(), c->rec_A.data(), L);
+    *stable = (h == 0 && c->stab_fired < 0) ? 1 : 0;
     if (!*stable) {  // rollback from the device snapshot; the noise counter is NOT rewound,
                      // so a retried frame draws fresh noise (as the reference's LCG state)
         for (auto &s : c->slabs)
@@ -1063,6 +1163,8 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->dacc);
     (void)hipFree(c->dtune);
     (void)hipFree(c->dmax);
+    (void)hipFree(c->st_md);
+    (void)hipFree(c->st_a);
     if (c->qstream) (void)hipStreamDestroy(c->qstream);
     for (auto &e : c->evpool) {
         (void)hipEventDestroy(e.a);
@@ -1255,6 +1357,33 @@ int sq_phi4_ghost(sq_ctx *c, int *active, int *allocated) {
     return SQ_OK;
 }
 
+int sq_phi4_stability(sq_ctx *c, double state[2], int *fired_step, float *M, float *D, float *A, int n) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (n < 0 || (n > 0 && (!M || !D || !A))) return fail(SQ_E_ARG, "bad record arguments");
+    if (n > (int)c->rec_M.size()) return fail(SQ_E_ARG, "n exceeds the last frame's steps");
+    if (state) {
+        state[0] = c->stab_T;
+        state[1] = c->stab_V;
+    }
+    if (fired_step) *fired_step = c->stab_fired;
+    for (int j = 0; j < n; ++j) {
+        M[j] = c->rec_M[j];
+        D[j] = c->rec_D[j];
+        A[j] = c->rec_A[j];
+    }
+    return SQ_OK;
+}
+
+int sq_phi4_set_stability(sq_ctx *c, double T, double V) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    c->stab_T = (float)T;
+    c->stab_V = (float)V;
+    c->stab_init = true;
+    return SQ_OK;
+}
+
 int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
                        int *nops) {
     if (!nops || (cap > 0 && !ops)) return fail(SQ_E_ARG, "null argument");
@@ -1332,7 +1461,7 @@ int sq_moments(sq_ctx *c, double out[3]) {
     out[0] = out[1] = out[2] = 0;
     for (auto &s : c->slabs) {
         SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));  // same stream as the kernel:
-        SQ_HIP(hipMemsetAsync(c->dmax, 0, sizeof(unsigned int), s.sA));  // the null stream does not order non-blocking streams
+        SQ_HIP(hipMemsetAsync(c->dmax, 0, 2 * sizeof(unsigned int), s.sA));  // the null stream does not order non-blocking streams
         SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane,
                                        c->dacc, c->dmax, s.sA));
         double acc[2];

@@ -28,8 +28,15 @@ struct Phi4StepArgs {
     long long Lzg;            // global Lz (the noise index of ghost-zone planes wraps)
     float h, m2, lam6, sig, clampv;
     uint32_t k0, k1, s_lo, s_hi;
-    int *flag;                // guard flag: set to 1 when a site was clamped / NaN (nullable)
+    int *flag;                // guard flag: set to 1 when a site was clamped / NaN (nullable: frames only)
+    // stability records of this launch's step(s) (nullable; frames only): for
+    // step k of the launch, kStabSlots words each at st_md + k*kStabSlots
+    // (u64 max of ord(max phi') << 32 | bits(drift increment there)) and
+    // st_a + k*kStabSlots (u32 max of bits(max |phi'|)); DESIGN.md §7
+    unsigned long long *st_md;
+    unsigned int *st_a;
 };
+constexpr int kStabSlots = 32;
 
 struct Phi4Geom {
     int qx;   // lanes per x segment (4 sites each)
@@ -60,8 +67,9 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
 // slab = local plane 0 (past the ghost zone)
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
-// Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2, acc[2] = max |phi| (as
-// ordered-int bits in acc_max).  acc must be zeroed by the caller.
+// Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2; acc_max[0] = max
+// |phi| (float bits), acc_max[1] = max phi (order-preserving bits, see
+// sq_phi4.hip ord_f32).  acc and acc_max must be zeroed by the caller.
 hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max,
                                hipStream_t s);
 // Slice sums S(z) = sum_{x,y} phi(x,y,z) for z in [0,nz): out[z] (double); slab = local plane 0.

@@ -120,6 +120,80 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
                        fmaxf(fminf(v1.y, cl), -cl));
 }
 
+// Per-lane frame accumulators (frames only, A.flag != nullptr): the guard
+// flag of tau_kernel.cl:119-133 and, per step, the record of the stability
+// heuristic (tau_kernel.cl:135-143): m = max phi', d = the
+// drift increment |phi' - phi - sigma xi| at the sites attaining m (the
+// largest one on ties), a = max |phi'|.
+struct FrameAcc {
+    int bad;
+    float m, d, a;
+};
+__device__ __forceinline__ FrameAcc frame_acc() { return FrameAcc{0, -__builtin_inff(), 0.f, 0.f}; }
+
+__device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float xi, float sig) {
+    const float dn = fabsf(__builtin_fmaf(-sig, xi, o - c));
+    f.d = o > f.m ? dn : (o == f.m ? fmaxf(f.d, dn) : f.d);
+    f.m = fmaxf(f.m, o);
+    f.a = fmaxf(f.a, fabsf(o));
+}
+
+// The frame bookkeeping of one float4 of outputs o (inputs c, noise xi).
+template <bool NZ>
+__device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
+                                            const f32x4n &xi) {
+    const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+    f.bad |= (int)(m >= A.clampv);
+    if (A.st_md != nullptr) {
+        const float s = NZ ? A.sig : 0.f;
+        stab_site(f, o.x, c.x, xi.a, s);
+        stab_site(f, o.y, c.y, xi.b, s);
+        stab_site(f, o.z, c.z, xi.c, s);
+        stab_site(f, o.w, c.w, xi.d, s);
+    }
+}
+
+// Order-preserving float -> uint map (the stability records are u64 maxima of
+// (ord(m) << 32) | bits(d): the larger m wins, equal m the larger d).
+__device__ __forceinline__ uint32_t ord_f32(float v) {
+    const uint32_t u = __float_as_uint(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Block-wide reduction of the frame accumulators, one atomic per block and
+// step record (slot = block % kStabSlots spreads them over kStabSlots words);
+// every wave of the block must call it.
+__device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAcc &f, int rec, uint64_t *sk,
+                                            uint32_t *sa) {
+    if (__ballot(f.bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    if (A.st_md == nullptr) return;
+    uint64_t k = ((uint64_t)ord_f32(f.m) << 32) | __float_as_uint(f.d);
+    uint32_t a = __float_as_uint(f.a);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t k2 = __shfl_xor(k, o, 64);
+        const uint32_t a2 = __shfl_xor(a, o, 64);
+        k = k2 > k ? k2 : k;
+        a = a2 > a ? a2 : a;
+    }
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sk[w] = k;
+        sa[w] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int i = 1; i < nw; ++i) {
+            k = sk[i] > k ? sk[i] : k;
+            a = sa[i] > a ? sa[i] : a;
+        }
+        const int slot = rec * kStabSlots + (int)(blockIdx.x % kStabSlots);
+        atomicMax(A.st_md + slot, (unsigned long long)k);
+        atomicMax(A.st_a + slot, a);
+    }
+}
+
 // Philox4x32-10 on R independent counters, round-major so the R dependency
 // chains interleave; the three-input xors are one v_bitop3_b32 each.
 template <int R>
@@ -179,11 +253,12 @@ __device__ __forceinline__ void load_slot(const Phi4StepArgs &A, const Lane<QX, 
 // MS: the row spans several wave x-spans (Lx > 256 V): the span's two outer
 //     neighbours come from scalar loads by lanes 0 / 63.
 // NZ: noise on (C != 0); off, the C = 0 gradient flow skips the RNG.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX, bool FR>
 __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                               const Slot<R, V> &P, const Slot<R, V> &C,
                                               const Slot<R, V> &N, int z, size_t plane,
-                                              uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
+                                              uint32_t pbytes, uint32_t qplane, uint32_t slo, uint32_t shi,
+                                              FrameAcc &fa) {
     float el[R], er[R];
     if constexpr (MS) {
         const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, padded_index(A, z), plane, pbytes);
@@ -260,29 +335,28 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
                 o.z = site_update<NZ>(cc.z, cc.y, cc.w, up.z, dn.z, P.row[k].z, N.row[k].z, xi[k].c, A);
                 o.w = site_update<NZ>(cc.w, cc.z, rgt, up.w, dn.w, P.row[k].w, N.row[k].w, xi[k].d, A);
             }
-            if (A.flag != nullptr) {  // frames only: raw sq_step has no rollback to feed
-                const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-                bad |= (int)(m >= A.clampv);
-            }
+            // frames only: raw sq_step has no rollback to feed (lanes past Ly
+            // compute duplicates of rows 0.., which change no maximum)
+            if constexpr (FR) frame_sites<NZ>(A, fa, o, cc, xi[k]);
             if (L.rows_ok) bstore4<SAUX>(ws, L.voff[k], o);
         }
     }
 }
 
 // Prefetch distance 1: load plane z+1 into N, then update plane z.
-template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX = 0>
+template <int QX, int R, int V, bool MS, bool NZ, bool PK, int SAUX, bool FR>
 __device__ __forceinline__ void plane_step(const Phi4StepArgs &A, const Lane<QX, R, V> &L,
                                            const Slot<R, V> &P, const Slot<R, V> &C, Slot<R, V> &N,
                                            int z, int zend, size_t plane, uint32_t pbytes,
-                                           uint32_t qplane, uint32_t slo, uint32_t shi, int &bad) {
+                                           uint32_t qplane, uint32_t slo, uint32_t shi, FrameAcc &fa) {
     load_slot<QX, R, V>(A, L, N, z + 1, z + 1 < zend, plane, pbytes);
-    plane_compute<QX, R, V, MS, NZ, PK, SAUX>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, bad);
+    plane_compute<QX, R, V, MS, NZ, PK, SAUX, FR>(A, L, P, C, N, z, plane, pbytes, qplane, slo, shi, fa);
 }
 
 // One wave's unit of a step: an x-span of 4*QX*V sites by R row sets by a
 // z-chunk.
-template <int QX, int R, int V, bool MS, bool NZ, int PF>
-__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, int &bad, uint32_t slo, uint32_t shi) {
+template <int QX, int R, int V, bool MS, bool NZ, int PF, bool FR>
+__device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, FrameAcc &fa, uint32_t slo, uint32_t shi) {
     constexpr int RS = 64 / QX;  // row sets per wave
     // x-segments fastest, then y-groups: the waves that share a row's segment
     // edges (MS) and the y-halo rows are consecutive units, i.e. the same or
@@ -334,7 +408,6 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, int &b
     Slot<R, V> S0, S1, S2;
     load_slot<QX, R, V>(A, L, S0, zbeg - 1, false, plane, pbytes);
     load_slot<QX, R, V>(A, L, S1, zbeg, true, plane, pbytes);
-    int ubad = 0;
     // three-slot register queue, unrolled so no rotation moves are needed.
     // PF 3: packed-f32 site arithmetic, plain stores; 4: non-temporal output
     // stores, for lattices whose two fields exceed the Infinity Cache (512^3
@@ -346,26 +419,28 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, int &b
     constexpr bool PK = PF >= 3;
     constexpr int SAUX = PF == 4 ? 2 : PF == 7 ? 17 : 0;
     for (int z = zbeg; z < zend; z += 3) {
-        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, slo, shi, ubad);
+        plane_step<QX, R, V, MS, NZ, PK, SAUX, FR>(A, L, S0, S1, S2, z, zend, plane, pbytes, qplane, slo, shi, fa);
         if (z + 1 >= zend) break;
-        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, ubad);
+        plane_step<QX, R, V, MS, NZ, PK, SAUX, FR>(A, L, S1, S2, S0, z + 1, zend, plane, pbytes, qplane, slo, shi, fa);
         if (z + 2 >= zend) break;
-        plane_step<QX, R, V, MS, NZ, PK, SAUX>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, ubad);
+        plane_step<QX, R, V, MS, NZ, PK, SAUX, FR>(A, L, S2, S0, S1, z + 2, zend, plane, pbytes, qplane, slo, shi, fa);
     }
-    if (L.rows_ok) bad |= ubad;
 }
 
-template <int QX, int R, int V, bool MS, bool NZ, int PF>
+// FR: a frame's launch (guard flag and stability records); the raw sq_step
+// path compiles without that bookkeeping.
+template <int QX, int R, int V, bool MS, bool NZ, int PF, bool FR>
 __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
     // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
     const int unit = __builtin_amdgcn_readfirstlane(lb * 4 + (int)(threadIdx.x >> 6));
-    if (unit >= A.nunits) return;
-    int bad = 0;
-    unit_run<QX, R, V, MS, NZ, PF>(A, unit, bad, A.s_lo, A.s_hi);
-    if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    FrameAcc fa = frame_acc();
+    if (unit < A.nunits) unit_run<QX, R, V, MS, NZ, PF, FR>(A, unit, fa, A.s_lo, A.s_hi);
+    if constexpr (FR) {  // every wave of the block, finished or idle, reaches the flush
+        __shared__ uint64_t sk[4];
+        __shared__ uint32_t sa[4];
+        frame_flush(A, fa, 0, sk, sa);
     }
 }
 
@@ -460,10 +535,11 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
 // One plane of the march.  Row waves: I0 (p-1), I1 (p), I2 (p+1, loaded
 // here); T0 (p-2), T1 (p-1), T2 (p, computed here).  The x-halo wave: the
 // centres of its sites at the same planes in row.x.
-template <bool NZ, bool WIDE>
+template <bool NZ, bool WIDE, bool FR>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
-                                         float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], int &bad) {
+                                         float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
+                                         FrameAcc &f2) {
     const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, tb_pidx(A, p + 1), K.plane, K.pbytes);
     // S > 1: plane p's values at the segment's outer x-neighbours (lane 0 x0-1,
     // lane 63 x0+256) and at the x-halo sites' in-plane neighbours are loaded
@@ -482,10 +558,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             if (K.lane == 63) rgt = ex;
         }
         T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A);
-        if (A.flag != nullptr) {
-            const float m = fmaxf(fmaxf(fabsf(T2.x), fabsf(T2.y)), fmaxf(fabsf(T2.z), fabsf(T2.w)));
-            bad |= (int)(m >= A.clampv);
-        }
+        if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa);
         const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
         lds[sl][K.w][K.lane] = T2;
     } else {
@@ -509,10 +582,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             if (K.lane == 63) rgt = tx[sp][K.w][1];
         }
         const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A);
-        if (A.flag != nullptr) {
-            const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-            bad |= (int)(m >= A.clampv);
-        }
+        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb);
         const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
         bstore4<17>(ws, K.voff, o);
     }
@@ -523,7 +593,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 // 256-wide rows: 65 VGPRs, two 10-wave blocks per CU.  A 64-VGPR budget
 // (three blocks per CU) measured slower at every z-chunk
 // (profiles/r01/fuse2_sweep.log).
-template <bool NZ, bool WIDE, int WPE>
+template <bool NZ, bool WIDE, int WPE, bool FR>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A) {
     const int nb = gridDim.x, b = blockIdx.x;
@@ -592,17 +662,20 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         }
     }
     float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
-    int bad = 0;
+    FrameAcc f1 = frame_acc(), f2 = frame_acc();  // steps s and s+1
     // three-plane queues unrolled three ways so no rotation moves are emitted
     for (int p = K.z0 - 1; p <= z1; p += 3) {
-        tb_plane<NZ, WIDE>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, bad);
+        tb_plane<NZ, WIDE, FR>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
         if (p + 1 > z1) break;
-        tb_plane<NZ, WIDE>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, bad);
+        tb_plane<NZ, WIDE, FR>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
         if (p + 2 > z1) break;
-        tb_plane<NZ, WIDE>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, bad);
+        tb_plane<NZ, WIDE, FR>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
     }
-    if (A.flag != nullptr) {
-        if (__ballot(bad) != 0ull && K.lane == 0) atomicOr(A.flag, 1);
+    if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
+        __shared__ uint64_t sk[kTbWaves + 1];
+        __shared__ uint32_t sa[kTbWaves + 1];
+        frame_flush(A, f1, 0, sk, sa);
+        frame_flush(A, f2, 1, sk, sa);
     }
 }
 
@@ -633,7 +706,7 @@ __device__ __forceinline__ float wave_max(float v) {
 __global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long long n4,
                                                            double *acc, unsigned int *acc_max) {
     double s1 = 0, s2 = 0;
-    float mx = 0;
+    float mx = 0, mp = -__builtin_inff();
     const float4 *q = reinterpret_cast<const float4 *>(p);
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (long long)gridDim.x * blockDim.x) {
@@ -641,30 +714,35 @@ __global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long 
         s1 += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
         s2 += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
         mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+        mp = fmaxf(mp, fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w)));
     }
     __shared__ double sh1[4], sh2[4];
-    __shared__ float shm[4];
+    __shared__ float shm[4], shp[4];
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
     mx = wave_max(mx);
+    mp = wave_max(mp);
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0) {
         sh1[w] = s1;
         sh2[w] = s2;
         shm[w] = mx;
+        shp[w] = mp;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         double t1 = 0, t2 = 0;
-        float tm = 0;
+        float tm = 0, tp = -__builtin_inff();
         for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
             t1 += sh1[k];
             t2 += sh2[k];
             tm = fmaxf(tm, shm[k]);
+            tp = fmaxf(tp, shp[k]);
         }
         atomicAdd(&acc[0], t1);
         atomicAdd(&acc[1], t2);
         atomicMax(acc_max, __float_as_uint(tm));
+        atomicMax(acc_max + 1, ord_f32(tp));
     }
 }
 
@@ -728,14 +806,20 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g) {
     a.nunits = a.nxseg * a.nyg * a.nzc;
 }
 
+template <int QX, int R, int V, bool MS, bool NZ, int PF, bool FR>
+static hipError_t launch_fr(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF, FR>), grid, dim3(256), 0, s, e0, e1, 0, a);
+    else
+        hipLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF, FR>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
 template <int QX, int R, int V, bool MS, bool NZ, int PF>
 static hipError_t launch_pf(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
                             hipEvent_t e1) {
-    if (e0 != nullptr || e1 != nullptr)
-        hipExtLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF>), grid, dim3(256), 0, s, e0, e1, 0, a);
-    else
-        hipLaunchKernelGGL((phi4_step_kernel<QX, R, V, MS, NZ, PF>), grid, dim3(256), 0, s, a);
-    return hipGetLastError();
+    return a.flag != nullptr ? launch_fr<QX, R, V, MS, NZ, PF, true>(a, grid, s, e0, e1)
+                             : launch_fr<QX, R, V, MS, NZ, PF, false>(a, grid, s, e0, e1);
 }
 
 template <int QX, int R, int V, bool MS>
@@ -798,13 +882,16 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     const dim3 grid((unsigned)a.nunits), block((kTbWaves + (wide ? 1 : 0)) * 64);
     const bool nz = a.sig != 0.0f;
     static const int wpe = getenv("SQ_TB2_WPE") ? atoi(getenv("SQ_TB2_WPE")) : 6;
+    const bool fr = a.flag != nullptr;
     const void *fn;
+#define SQ_TB2(N, W, E) (fr ? (const void *)&phi4_tb2_kernel<N, W, E, true> : (const void *)&phi4_tb2_kernel<N, W, E, false>)
     if (wide && wpe == 6)
-        fn = nz ? (const void *)&phi4_tb2_kernel<true, true, 6> : (const void *)&phi4_tb2_kernel<false, true, 6>;
+        fn = nz ? SQ_TB2(true, true, 6) : SQ_TB2(false, true, 6);
     else if (wide)
-        fn = nz ? (const void *)&phi4_tb2_kernel<true, true, 1> : (const void *)&phi4_tb2_kernel<false, true, 1>;
+        fn = nz ? SQ_TB2(true, true, 1) : SQ_TB2(false, true, 1);
     else
-        fn = nz ? (const void *)&phi4_tb2_kernel<true, false, 1> : (const void *)&phi4_tb2_kernel<false, false, 1>;
+        fn = nz ? SQ_TB2(true, false, 1) : SQ_TB2(false, false, 1);
+#undef SQ_TB2
     Phi4StepArgs q = a;
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);

@@ -273,6 +273,20 @@ class Phi4Lattice(_Ctx):
     def load(self, path, restore_counters=True):
         _lib.call("sq_load_field", self._h, os.fsencode(path), 1 if restore_counters else 0)
 
+    def stability(self, n=None):
+        """The frame stability heuristic's state: {"T", "V", "fired" (step of the
+        last frame it fired at, -1 none), "M", "D", "A" (that frame's per-step
+        records)} -- DESIGN.md §7."""
+        n = self.params.loops if n is None else int(n)
+        st = np.zeros(2)
+        fired = ctypes.c_int()
+        M, D, A = (np.zeros(n, dtype=np.float32) for _ in range(3))
+        _lib.call("sq_phi4_stability", self._h, _dptr(st), ctypes.byref(fired), _fptr(M), _fptr(D), _fptr(A), n)
+        return {"T": st[0], "V": st[1], "fired": fired.value, "M": M, "D": D, "A": A}
+
+    def set_stability(self, T, V):
+        _lib.call("sq_phi4_set_stability", self._h, float(T), float(V))
+
     def correlator(self, n=None):
         n = self.shape[2] if n is None else int(n)
         out = np.empty(n)

@@ -590,3 +590,60 @@ def test_checkpoint_load_validates_before_touching_the_field(gpu, oracle_mod, tm
             assert L.step_counter == 7
         L.load(tmp_path / "seed" / "ck.npy", restore_counters=False)   # a field as an initial condition
         assert L.step_counter == 7
+
+
+STAB_CASES = [((256, 8, 8), {}), ((64, 16, 8), {}), ((512, 8, 6), {"SQ_FUSE2": "1"}),
+              ((256, 8, 12), {"comm": "loopback", "nslabs": 3}), ((256, 16, 16), {"comm": "rccl"})]
+
+
+@pytest.mark.parametrize("shape,opt", STAB_CASES)
+def test_stability_rule_rolls_back_diverging_unclamped_field(gpu, oracle_mod, monkeypatch, shape, opt):
+    """The reference's stability heuristic (tau_kernel.cl:135-143) restated for
+    the 3-D lattice: Euler at dtau = 0.2 > 2/lambda_max diverges
+    as an oscillation that stays far below the clamp within the frame, so only
+    the heuristic can catch it.  Per-step records (M, D, A), the firing step,
+    the carried T / V and the rollback are bit-identical to the oracle's
+    statement of the same rule (C = 0), through the fused, per-step,
+    multi-segment, loopback-slab and RCCL-slab paths."""
+    from stochquant_amd import unique_id
+    kw = dict(opt)
+    for k in [k for k in kw if k.startswith("SQ_")]:
+        monkeypatch.setenv(k, kw.pop(k))
+    if kw.get("comm") == "rccl":
+        kw.update(nranks=1, rank=0, comm_id=unique_id())
+        monkeypatch.setenv("SQ_GHOST", "4")
+    loops, h = 12, 0.2
+    phi0 = _init(oracle_mod, shape, amp=0.05)
+    p = oracle_mod.phi4_params(shape, h, 1.0, 1.0, 1234, C=0.0)
+    T0, V0 = float(phi0.max()), float(np.abs(phi0).max())
+    out, M, D, A, fired, T1, V1 = oracle_mod.phi4_frame_stab(p, phi0, loops, 0, T0, V0)
+    assert fired >= 0 and np.abs(out).max() < 1000        # diverging, never clamped
+    with _lat(shape, C=0.0, dtau=h, m2=1.0, lam=1.0, loops=loops, **kw) as L:
+        L.upload(phi0)
+        assert not L.run_frame()
+        st = L.stability()
+        assert np.array_equal(st["M"], M) and np.array_equal(st["D"], D) and np.array_equal(st["A"], A)
+        assert st["fired"] == fired and st["T"] == T1 and st["V"] == V1
+        assert np.array_equal(L.download(), phi0)           # rolled back
+        assert L.dtau == pytest.approx(h * 0.95)
+        assert L.step_counter == loops                      # a retried frame draws fresh noise
+
+
+def test_stability_rule_quiet_on_stable_frames(gpu, oracle_mod):
+    """dtau = 0.01, noise on: the heuristic never fires, records within the
+    noise tolerance of the oracle's (hardware transcendentals in xi)."""
+    shape, loops = (256, 16, 16), 6
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    p = oracle_mod.phi4_params(shape, 0.01, 1.0, 1.0, 1234, C=1.0)
+    out, M, D, A, fired, T1, V1 = oracle_mod.phi4_frame_stab(p, phi0, loops, 0, float(phi0.max()),
+                                                            float(np.abs(phi0).max()))
+    assert fired == -1
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, loops=loops) as L:
+        L.upload(phi0)
+        assert L.run_frame()
+        st = L.stability()
+        assert st["fired"] == -1
+        tol = loops * (STEP_ATOL + STEP_RTOL * 4.0)
+        assert np.allclose(st["M"], M, atol=tol) and np.allclose(st["A"], A, atol=tol)
+        assert np.allclose(st["D"], D, atol=tol)
+        assert np.allclose(L.download(), out, atol=tol)
