@@ -211,21 +211,21 @@ def main():
             break
     settle_ms = (time.perf_counter() - t_settle) * 1e3
     lat.step(a.warmup)
-    lat.sync()
-    torch.cuda.synchronize()
+    # host bookkeeping while the warm-up steps run, so the device idles only
+    # for the one synchronisation before the timed region (an idle gap lets the
+    # clocks drop again).  mode 2: ONE hipEvent pair on the step-kernel stream
+    # around the K timed launches (per-launch dispatch events cost ~4 us of wall
+    # per step); avg step = region / K, inter-kernel gaps included.
     lat.perf_reset()
-    # mode 2: ONE hipEvent pair on the step-kernel stream around the K timed
-    # launches (per-launch dispatch events cost ~4 us of wall per step, see
-    # DESIGN.md §6); avg launch = region / launches, inter-kernel gaps included.
     lat.set_profiling(0 if a.no_profile_events else 2)
-    barrier()
     torch.cuda.synchronize()
+    barrier()
     t0 = time.perf_counter()
     lat.step(a.steps)
-    lat.sync()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()   # hipDeviceSynchronize: every stream of the library's slabs
     barrier()
     t = time.perf_counter() - t0
+    lat.sync()                 # the library's own join + error check, outside the timed region
     perf = lat.perf()
     lat.set_profiling(0)
     if world > 1:

@@ -45,11 +45,14 @@ def main():
     ap.add_argument("write_dir")
     ap.add_argument("--size", type=int, default=256)
     ap.add_argument("--nranks", type=int, default=1)
+    ap.add_argument("--kernel", default="phi4_tb2", help="kernel-name substring (phi4_tb2 or phi4_step)")
+    ap.add_argument("--sq", help="a pmc_sq_summary.py --json output of the same command: its issue "
+                                 "figures are recorded beside the traffic")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "pmc_traffic.json"))
     a = ap.parse_args()
-    fv, kname = counter_values(a.fetch_dir, "FETCH_SIZE")
-    wv, _ = counter_values(a.write_dir, "WRITE_SIZE")
+    fv, kname = counter_values(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    wv, _ = counter_values(a.write_dir, "WRITE_SIZE", a.kernel)
     # drop the first launches (cold caches) when there are enough samples
     fv_s = fv[len(fv) // 5:] if len(fv) >= 10 else fv
     wv_s = wv[len(wv) // 5:] if len(wv) >= 10 else wv
@@ -77,6 +80,23 @@ def main():
         "traffic_over_hbm_min": (read_bytes + write_bytes) / (8 * a.size ** 3),
         "correction": "FETCH_SIZE x2 (gfx950 reports half of wide streaming reads), KiB x1024",
     }
+    if a.sq:
+        with open(a.sq) as fh:
+            sq = json.load(fh)
+        med, der = sq["median_per_launch"], sq["derived"]
+        waves_per_simd = None
+        if "SQ_WAVES" in med:
+            # resident waves per SIMD: the grid is one round of blocks (bench), so
+            # every wave is resident for (nearly) the whole launch
+            waves_per_simd = med["SQ_WAVES"] / 1024.0
+        act = der.get("SQ_ACTIVE_INST_VALU/WAVE_CYCLES")
+        out["sq_source"] = a.sq
+        out["valu_insts_per_wave"] = der.get("VALU_insts_per_wave")
+        out["valu_active_per_wave"] = act
+        out["waves_per_simd"] = waves_per_simd
+        # each SIMD's VALU issue is busy ~ waves x the fraction of a wave's cycles it issues VALU
+        out["valu_issue_frac"] = round(min(1.0, act * waves_per_simd), 3) if act and waves_per_simd else None
+        out["valu_issue_frac_by_grbm"] = der.get("VALU_issue_frac_at_4cyc")
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

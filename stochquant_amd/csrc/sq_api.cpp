@@ -590,6 +590,7 @@ int create_phi4(sq_ctx *c) {
         return fail(SQ_E_ARG, "lattice exceeds 2^34 sites (Philox counter layout)");
     if ((long long)c->Lx * c->Ly * 4 >= (1ll << 31))
         return fail(SQ_E_ARG, "plane exceeds 2 GiB (32-bit buffer offsets)");
+    if (c->Lz >= (1ll << 31)) return fail(SQ_E_ARG, "Lz must be < 2^31 (32-bit plane indices)");
     if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
         const int r = atoi(e), rs = 64 / c->geom.qx;
         if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0)

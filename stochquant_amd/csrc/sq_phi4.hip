@@ -69,10 +69,13 @@ __device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
 }
 
 // Global z of local plane zl (ghost-zone planes of the first / last slab wrap).
-__device__ __forceinline__ long long global_z(const Phi4StepArgs &A, int zl) {
-    long long zg = A.zg0 + zl;
-    if (zg < 0) zg += A.Lzg;
-    else if (zg >= A.Lzg) zg -= A.Lzg;
+// 32-bit: Lz < 2^31 (create_phi4), so the wrap stays scalar (gfx950 has no
+// scalar 64-bit signed compare; the 64-bit form cost 4 VALU per plane).
+__device__ __forceinline__ int global_z(const Phi4StepArgs &A, int zl) {
+    const int Lz = (int)A.Lzg;
+    int zg = (int)A.zg0 + zl;
+    if (zg < 0) zg += Lz;
+    else if (zg >= Lz) zg -= Lz;
     return zg;
 }
 
