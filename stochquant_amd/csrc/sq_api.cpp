@@ -282,23 +282,29 @@ void count_step(sq_ctx *c) {
     for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane_floats(c);
 }
 
-// Steps s and s+1 on planes [zlo, zhi) of slab s in one launch
-// (sq_phi4.hip, phi4_tb2_kernel): reads buffer in_buf, writes in_buf ^ 1.
-int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo, int zhi, int periodic,
-                   bool timed) {
-    if (zhi <= zlo) return SQ_OK;
+// Steps s and s+1 in one launch (sq_phi4.hip, phi4_tb2_kernel) on the planes
+// [lo, hi) of slab s and, when lo2 < hi2, also [lo2, hi2) (a range of the same
+// length): reads buffer in_buf, writes in_buf ^ 1.
+int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo, int hi, int lo2, int hi2,
+                   int periodic, bool timed) {
+    if (hi <= lo) return SQ_OK;
+    const int nr = lo2 < hi2 ? 2 : 1, len = hi - lo;
+    if (nr == 2 && hi2 - lo2 != len) return fail(SQ_E_STATE, "two-step launch: ranges of different lengths");
     sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
     // planes per block: pinned, or as many as make one round of tb_blocks
-    // blocks (a ragged second round costs more than the deeper chunks)
-    const int nyg = c->Ly / 8, nxseg = c->Lx / 256, span = zhi - zlo;
+    // blocks (a ragged second round costs more than the deeper chunks), but
+    // not fewer than 4 (a chunk recomputes 2 planes of the first step)
+    const int nyg = c->Ly / 8, nxseg = c->Lx / 256;
     // (the slabs of a loopback decomposition run concurrently on their own streams)
-    const int nzc_t = std::max(1, c->tb_blocks / (nyg * nxseg * (int)c->slabs.size()));
-    const int zb = c->tbz_pin ? c->tbz : std::max(1, (span + nzc_t - 1) / nzc_t);
-    a.zlo = zlo;
-    a.zhi = zhi;
-    a.zstep = zb;
+    const int nzc_t = std::max(1, c->tb_blocks / (nyg * nxseg * (int)c->slabs.size() * nr));
+    const int zb = c->tbz_pin ? c->tbz : std::min(len, std::max(4, (len + nzc_t - 1) / nzc_t));
+    a.zlo = lo;
+    a.zhi = nr == 2 ? hi2 : hi;
+    a.zstep = nr == 2 ? lo2 - lo : 0;
     a.zc = zb;
-    a.nzc = (span + zb - 1) / zb;
+    a.zlen = len;
+    a.nzr = (len + zb - 1) / zb;
+    a.nzc = nr * a.nzr;
     a.periodic = periodic;
     a.nxseg = nxseg;
     a.nyg = nyg;
@@ -319,7 +325,7 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int zlo
 // output lands in the other buffer.
 int phi4_tb2_pair(sq_ctx *c) {
     Slab &s = c->slabs[0];
-    int rc = phi4_tb2_range(c, s, c->cur, s.sA, 0, s.nz, 1, true);
+    int rc = phi4_tb2_range(c, s, c->cur, s.sA, 0, s.nz, 0, 0, 1, true);
     if (rc) return rc;
     c->cur ^= 1;
     count_step(c);
@@ -342,14 +348,17 @@ int phi4_periodic_step(sq_ctx *c) {
 // with a ghost zone of G planes:
 //   EXCHANGE     stream B, after the previous block's EDGES_DONE: G edge planes
 //                of the block's input field to both z-neighbours, their ghosts in;
-//   STEP 0 core  [1, nz-1), the planes that need no ghost: overlaps the exchange;
-//   WAIT_EXCHANGE, STEP 0 rim [-(g-1), 1) u [nz-1, nz+g-1) (one launch);
-//   steps 1 .. g-1 on the shrinking extended range [-(g-1-s), nz+g-1-s): with
-//   fuse2, the steps before the last go in pairs (s, s+1) that write step
-//   s+1's range [-(g-2-s), nz+g-2-s) and read step s-1's, both inside the
-//   ghost zone; the last step computes its edge planes [0, G) u [nz-G, nz)
-//   first and marks EDGES_DONE, so the NEXT block's exchange overlaps this
-//   step's middle as well as the next core.
+//   then stream A.  Step k updates the shrinking extended range
+//   [-(g-1-k), nz+g-1-k), recomputing ghost-zone sites.  With fuse2 (two steps
+//   per launch) and g >= 3 every step runs in pairs:
+//     PAIR 0 core   step 1 on [2, nz-2): reads only [0, nz), so it overlaps the exchange;
+//     WAIT_EXCHANGE, PAIR 0 rim: step 1 on [-(g-2), 2) u [nz-2, nz+g-2) (one launch);
+//     PAIR s        steps s, s+1 on step s+1's range, reading step s-1's;
+//     the last pair (or single step) computes its edge planes [0, G) u
+//     [nz-G, nz) first and marks EDGES_DONE, so the NEXT block's exchange
+//     overlaps this step's middle as well as the next core;
+//   without fuse2 (or g < 3) step 0 is a single-step core [1, nz-1) / rim
+//   [-(g-1), 1) u [nz-1, nz+g-1) split and the later steps single launches.
 // Ghost-zone sites are recomputed redundantly; the counter-based noise makes
 // them bit-identical to their owner's, so the result equals the monolithic run.
 std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first) {
@@ -357,32 +366,43 @@ std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_
     auto add = [&](int kind, int step, int lo, int hi, int lo2 = 0, int hi2 = 0) {
         ops.push_back(sq_block_op{kind, step, lo, hi, lo2, hi2});
     };
+    const bool split_edges = edge_first && nz > 2 * G;
     add(SQ_OP_EXCHANGE, 0, 0, 0);
-    if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1);
-    add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
-    const int lo_a = -(g - 1), hi_a = 1, lo_b = nz - 1, hi_b = nz + g - 1;
-    if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
-        add(SQ_OP_STEP, 0, lo_a, hi_b);
-    else
-        add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b);
+    int st;
+    if (fuse2 && g >= 3) {
+        if (nz > 4) add(SQ_OP_PAIR, 0, 2, nz - 2);
+        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
+        const int lo_a = -(g - 2), hi_a = 2, lo_b = nz - 2, hi_b = nz + g - 2;
+        if (hi_a >= lo_b)  // rims meet (nz <= 4): one span
+            add(SQ_OP_PAIR, 0, lo_a, hi_b);
+        else
+            add(SQ_OP_PAIR, 0, lo_a, hi_a, lo_b, hi_b);
+        st = 2;
+    } else {
+        if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1);
+        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
+        const int lo_a = -(g - 1), hi_a = 1, lo_b = nz - 1, hi_b = nz + g - 1;
+        if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
+            add(SQ_OP_STEP, 0, lo_a, hi_b);
+        else
+            add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b);
+        st = 1;
+    }
     bool edges = false;
-    for (int st = 1; st < g;) {
-        if (fuse2 && st + 1 < g - 1) {
-            const int e = g - 2 - st;  // ghost planes step st+1 still updates on either side
-            add(SQ_OP_PAIR, st, -e, nz + e);
-            st += 2;
-            continue;
-        }
-        if (st == g - 1 && edge_first && nz > 2 * G) {
-            add(SQ_OP_STEP, st, 0, G);
-            add(SQ_OP_STEP, st, nz - G, nz);
+    while (st < g) {
+        const bool pair = fuse2 && st + 1 <= g - 1;
+        const int last = pair ? st + 1 : st;  // the step this op group completes
+        const int kind = pair ? SQ_OP_PAIR : SQ_OP_STEP;
+        if (last == g - 1 && split_edges) {
+            add(kind, st, 0, G, nz - G, nz);
             add(SQ_OP_EDGES_DONE, st, 0, 0);
-            add(SQ_OP_STEP, st, G, nz - G);
+            add(kind, st, G, nz - G);
             edges = true;
         } else {
-            add(SQ_OP_STEP, st, -(g - 1 - st), nz + (g - 1 - st));
+            const int e = g - 1 - last;  // ghost planes the completed step still updates on either side
+            add(kind, st, -e, nz + e);
         }
-        ++st;
+        st = last + 1;
     }
     if (!edges) add(SQ_OP_EDGES_DONE, g - 1, 0, 0);
     return ops;
@@ -441,41 +461,35 @@ int phi4_block(sq_ctx *c, int g) {
         Slab &s = c->slabs[i];
         const std::vector<sq_block_op> ops = block_plan(s.nz, G, g, c->tbz > 0, c->edge_first);
         int in = cur;            // buffer holding the latest completed step
-        bool flip = false;       // a STEP op of the current step wrote in ^ 1
-        int last = -1;           // step of the previous STEP op
+        bool flip = false;       // the current op group writes in ^ 1
+        int gstep = -1, gkind = -1;  // the current op group: ops of one kind and step read the same buffer
         for (const sq_block_op &op : ops) {
             int rc = SQ_OK;
-            switch (op.kind) {
-            case SQ_OP_EXCHANGE: break;  // issued above for every slab
-            case SQ_OP_WAIT_EXCHANGE:
+            if (op.kind == SQ_OP_STEP || op.kind == SQ_OP_PAIR) {
+                const bool first = op.step != gstep || op.kind != gkind;  // it carries the group's timing
+                if (first) {
+                    if (flip) in ^= 1;
+                    flip = true;
+                    gstep = op.step;
+                    gkind = op.kind;
+                }
+                c->step = step0 + (unsigned long long)op.step;
+                if (op.kind == SQ_OP_PAIR)
+                    rc = phi4_tb2_range(c, s, in, s.sA, op.lo, op.hi, op.lo2, op.hi2, 0, first);
+                else if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
+                    rc = phi4_launch_range(c, s, in, s.sA, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
+                else
+                    rc = phi4_launch_span(c, s, in, s.sA, op.lo, op.hi, first);
+            } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
                 SQ_HIP(hipStreamWaitEvent(s.sA, s.evC, 0));
                 if (c->p.comm == SQ_COMM_LOOPBACK) {
                     SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
                     SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
                 }
-                break;
-            case SQ_OP_EDGES_DONE: SQ_HIP(hipEventRecord(s.evE, s.sA)); break;
-            case SQ_OP_STEP: {
-                if (op.step != last && flip) in ^= 1;
-                const bool first = op.step != last;  // the first launch of a step carries its timing
-                flip = true;
-                last = op.step;
-                c->step = step0 + (unsigned long long)op.step;
-                if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
-                    rc = phi4_launch_range(c, s, in, s.sA, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
-                else
-                    rc = phi4_launch_span(c, s, in, s.sA, op.lo, op.hi, first);
-                break;
-            }
-            case SQ_OP_PAIR:
-                if (flip) in ^= 1;
-                flip = false;
-                last = op.step + 1;
-                c->step = step0 + (unsigned long long)op.step;
-                rc = phi4_tb2_range(c, s, in, s.sA, op.lo, op.hi, 0, true);
-                in ^= 1;
-                break;
-            default: return fail(SQ_E_STATE, "unknown block op");
+            } else if (op.kind == SQ_OP_EDGES_DONE) {
+                SQ_HIP(hipEventRecord(s.evE, s.sA));
+            } else if (op.kind != SQ_OP_EXCHANGE) {  // the exchange was issued above for every slab
+                return fail(SQ_E_STATE, "unknown block op");
             }
             if (rc) return rc;
         }

@@ -22,6 +22,8 @@ struct Phi4StepArgs {
     float *out;
     int Lx, Ly, nz, gz;            // gz: ghost planes allocated on either side (local plane 0 is padded plane gz)
     int zlo, zhi, zstep, zc, nzc;  // chunk k updates planes [zlo + k*zstep, +zc) clipped to zhi
+    int nzr, zlen;                 // two-step kernel: chunks per range and range length; chunk k covers
+                                   // [r0 + (k % nzr)*zc, +zc) clipped to r0 + zlen, r0 = zlo + (k / nzr)*zstep
     int periodic;
     int nxseg, nyg, nunits;
     long long zg0;            // global z of local plane 0
@@ -48,10 +50,12 @@ struct Phi4Geom {
     int v;    // float4 segments per lane per row (x-span of a wave = 4*qx*v sites): 1 or 2
 };
 
-// Two steps per launch (steps s and s+1, s = a.s_hi:a.s_lo) on planes
-// [a.zlo, a.zhi) (a single periodic slab: [0, nz)): a.zc = output planes per
-// block, a.nyg = Ly / 8 y-bands, a.nzc z-chunks, a.nunits = blocks; the
-// input must be valid on [zlo-2, zhi+2).  Bit-identical to two step launches.
+// Two steps per launch (steps s and s+1, s = a.s_hi:a.s_lo) on one or more
+// equal ranges of planes: range r = [zlo + r*zstep, + zlen) (a single periodic
+// slab: [0, nz)); a.zc = output planes per block, a.nzr chunks per range,
+// a.nzc = all chunks, a.nxseg = Lx / 256, a.nyg = Ly / 8 y-bands, a.nunits =
+// blocks; the input must be valid two planes beyond every range.
+// Bit-identical to two step launches.
 bool phi4_tb2_supported(int Lx, int Ly);
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t start = nullptr,
                            hipEvent_t stop = nullptr);

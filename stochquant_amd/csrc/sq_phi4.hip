@@ -612,8 +612,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     K.lane = threadIdx.x & 63;
     K.outw = K.w >= 1 && K.w <= kTbRows;
-    K.z0 = A.zlo + zk * A.zc;
-    const int z1 = min(K.z0 + A.zc, A.zhi);
+    const int r0 = A.zlo + (zk / A.nzr) * A.zstep;  // this chunk's range
+    K.z0 = r0 + (zk % A.nzr) * A.zc;
+    const int z1 = min(K.z0 + A.zc, r0 + A.zlen);
     K.plane = (size_t)Lx * (size_t)Ly;
     K.pbytes = (uint32_t)(K.plane * sizeof(float));
     K.qplane = (uint32_t)(K.plane >> 2);
@@ -876,10 +877,13 @@ bool phi4_tb2_supported(int Lx, int Ly) { return Lx % 256 == 0 && Ly % kTbRows =
 
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0 || a.nxseg != a.Lx / 256 || a.nyg != a.Ly / kTbRows ||
-        a.nunits != a.nxseg * a.nyg * a.nzc || (long long)a.zc * a.nzc < (long long)(a.zhi - a.zlo))
+        a.nzr < 1 || a.nzc % a.nzr != 0 || a.nunits != a.nxseg * a.nyg * a.nzc || a.zlen < 1 ||
+        (long long)a.zc * a.nzr < a.zlen)
         return hipErrorInvalidValue;
-    if (a.periodic ? (a.nz < 2 || a.zlo != 0 || a.zhi != a.nz)
-                   : (a.zlo - 2 < -a.gz || a.zhi + 2 > a.nz + a.gz))  // input planes outside the buffer
+    const int nr = a.nzc / a.nzr, last_end = a.zlo + (nr - 1) * a.zstep + a.zlen;
+    if (nr > 1 && a.zstep < a.zlen) return hipErrorInvalidValue;  // ranges overlap
+    if (a.periodic ? (a.nz < 2 || a.zlo != 0 || a.zlen != a.nz || nr != 1)
+                   : (a.zlo - 2 < -a.gz || last_end + 2 > a.nz + a.gz))  // input planes outside the buffer
         return hipErrorInvalidValue;
     const bool wide = a.nxseg > 1;
     const dim3 grid((unsigned)a.nunits), block((kTbWaves + (wide ? 1 : 0)) * 64);

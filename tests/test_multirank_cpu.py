@@ -62,29 +62,35 @@ def _exchange(bufs, cur, nz, G, world, up, dn):
     b[G + nz:G + nz + G] = hi.numpy()
 
 
+def _ranges(op):
+    r = [(op["lo"], op["hi"])]
+    if op["lo2"] < op["hi2"]:
+        r.append((op["lo2"], op["hi2"]))
+    return r
+
+
 def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn):
-    """Execute one block's schedule; returns the buffer holding the result."""
-    inb, flip, last = cur, False, -1
+    """Execute one block's schedule as phi4_block does: consecutive STEP or
+    PAIR ops of one step form a group that reads the latest buffer and writes
+    the other; returns the buffer holding the result."""
+    inb, flip, gstep, gkind = cur, False, -1, None
     for op in plan:
         k = op["op"]
         if k == "exchange":
             _exchange(bufs, cur, nz, G, world, up, dn)
-        elif k == "step":
-            if op["step"] != last and flip:
-                inb ^= 1
-            flip, last = True, op["step"]
-            oracle.phi4_step_range(p, bufs[inb], bufs[inb ^ 1], G, op["lo"], op["hi"], z0, step0 + op["step"])
-            if op["lo2"] < op["hi2"]:
-                oracle.phi4_step_range(p, bufs[inb], bufs[inb ^ 1], G, op["lo2"], op["hi2"], z0,
-                                       step0 + op["step"])
-        elif k == "pair":
-            if flip:
-                inb ^= 1
-            flip, last = False, op["step"] + 1
-            mid = np.full_like(bufs[inb], np.nan)
-            oracle.phi4_step_range(p, bufs[inb], mid, G, op["lo"] - 1, op["hi"] + 1, z0, step0 + op["step"])
-            oracle.phi4_step_range(p, mid, bufs[inb ^ 1], G, op["lo"], op["hi"], z0, step0 + op["step"] + 1)
-            inb ^= 1
+        elif k in ("step", "pair"):
+            if op["step"] != gstep or k != gkind:
+                if flip:
+                    inb ^= 1
+                flip, gstep, gkind = True, op["step"], k
+            s = step0 + op["step"]
+            for lo, hi in _ranges(op):
+                if k == "step":
+                    oracle.phi4_step_range(p, bufs[inb], bufs[inb ^ 1], G, lo, hi, z0, s)
+                else:   # two steps in one launch: step s on [lo-1, hi+1) into scratch, s+1 on [lo, hi)
+                    mid = np.full_like(bufs[inb], np.nan)
+                    oracle.phi4_step_range(p, bufs[inb], mid, G, lo - 1, hi + 1, z0, s)
+                    oracle.phi4_step_range(p, mid, bufs[inb ^ 1], G, lo, hi, z0, s + 1)
         else:
             assert k in ("wait_exchange", "edges_done")
     return inb ^ 1 if flip else inb
@@ -148,6 +154,8 @@ def _monolithic(steps):
     (2, 9, False, True, 4),    # per-step inner launches
     (3, 8, True, False, 4),    # edges not first
     (2, 9, True, True, 8),     # deeper zone: pairs over 2 ghost planes
+    (2, 12, True, True, 2),    # G = 2: blocks of one core/rim step and one edges-first step
+    (3, 10, True, True, 8),    # G = 8 over slabs of 12 planes: rims of 8 planes, no edge split
     (1, 7, True, True, 4),     # single rank, self-exchange
 ])
 def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, oracle_mod):
@@ -169,18 +177,27 @@ def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, or
 
 
 def test_block_plan_shapes():
-    """The schedule's ranges: core/rim, shrinking pairs, edges first."""
+    """The schedule's ranges: fused blocks pair every step --
+    a core pair overlapping the exchange, a rim pair after it, pairs over the
+    shrinking ghost range, the last pair edges first; unfused blocks split
+    step 0 into core and rim and run the rest one step per launch."""
     from stochquant_amd.decomp import block_plan
     ops = block_plan(64, 16, 16)
-    assert [o["op"] for o in ops[:4]] == ["exchange", "step", "wait_exchange", "step"]
-    assert (ops[1]["lo"], ops[1]["hi"]) == (1, 63)
-    assert (ops[3]["lo"], ops[3]["hi"], ops[3]["lo2"], ops[3]["hi2"]) == (-15, 1, 63, 79)
-    pairs = [o for o in ops if o["op"] == "pair"]
-    assert [(o["step"], o["lo"], o["hi"]) for o in pairs] == [(s, -(14 - s), 64 + 14 - s) for s in range(1, 15, 2)]
-    tail = [o for o in ops if o["step"] == 15]
-    assert [(o["op"], o["lo"], o["hi"]) for o in tail] == [("step", 0, 16), ("step", 48, 64), ("edges_done", 0, 0),
-                                                           ("step", 16, 48)]
-    # every step 1..g-1 covered exactly once, the last one ghost-free
+    assert [o["op"] for o in ops[:4]] == ["exchange", "pair", "wait_exchange", "pair"]
+    assert (ops[1]["step"], ops[1]["lo"], ops[1]["hi"]) == (0, 2, 62)
+    assert (ops[3]["lo"], ops[3]["hi"], ops[3]["lo2"], ops[3]["hi2"]) == (-14, 2, 62, 78)
+    inner = [o for o in ops[4:] if o["op"] == "pair" and 0 < o["step"] < 14]
+    assert [(o["step"], o["lo"], o["hi"]) for o in inner] == [(s, -(14 - s), 64 + 14 - s) for s in range(2, 14, 2)]
+    tail = [o for o in ops if o["step"] == 14]
+    assert [(o["op"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in tail] == [
+        ("pair", 0, 16, 48, 64), ("edges_done", 0, 0, 0, 0), ("pair", 16, 48, 0, 0)]
+    # odd g: the last step single, edges first
+    ops = block_plan(40, 4, 3)
+    assert [(o["op"], o["step"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in ops] == [
+        ("exchange", 0, 0, 0, 0, 0), ("pair", 0, 2, 38, 0, 0), ("wait_exchange", 0, 0, 0, 0, 0),
+        ("pair", 0, -1, 2, 38, 41), ("step", 2, 0, 4, 36, 40), ("edges_done", 2, 0, 0, 0, 0),
+        ("step", 2, 4, 36, 0, 0)]
+    # unfused: every step 1..g-1 covered once, the last one ghost-free
     ops = block_plan(12, 4, 3, fuse2=False, edge_first=False)
     steps = [(o["step"], o["lo"], o["hi"]) for o in ops if o["op"] == "step"]
     assert steps == [(0, 1, 11), (0, -2, 1), (1, -1, 13), (2, 0, 12)]
