@@ -137,6 +137,8 @@ struct sq_ctx {
     int cur = 0;
     int *flag = nullptr;
     bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
+    bool field_finite = true;  // every plane of the current field has been through the guard (or
+                               // came from sq_init_field); false after a caller's upload / load
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;  // [0] max |phi| bits, [1] ordered max phi
@@ -232,6 +234,8 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.m2 = (float)c->p.m2;
     a.lam6 = (float)((double)(float)c->p.lambda / 6.0);
     a.sig = (float)(sqrt(2.0 * (double)h) * c->p.C);  // sigma = C*sqrt(2 dtau) (tau_kernel.cl:112, a = 1)
+    a.sigq = (float)(sqrt(2.0 * (double)h) * c->p.C * sq::kSqrt2Ln2);  // for the kernels' box_muller_q normals
+    a.fin = c->field_finite ? 1 : 0;
     a.clampv = (float)c->p.clamp;
     a.k0 = (uint32_t)c->p.seed;
     a.k1 = (uint32_t)(c->p.seed >> 32);
@@ -554,7 +558,18 @@ int phi4_autotune(sq_ctx *c, int &n) {
     return SQ_OK;
 }
 
+int phi4_steps_impl(sq_ctx *c, int n);
+
+// Every launch of the call reads c->field_finite as its `fin`; once one step
+// has run, every plane (ghost zones included: they are exchanged copies) has
+// been through the guard.
 int phi4_steps(sq_ctx *c, int n) {
+    const int rc = phi4_steps_impl(c, n);
+    if (rc == SQ_OK && n > 0) c->field_finite = true;
+    return rc;
+}
+
+int phi4_steps_impl(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
         for (; c->tbz > 0 && n >= 2; n -= 2) {
             int rc = phi4_tb2_pair(c);
@@ -605,6 +620,14 @@ int create_phi4(sq_ctx *c) {
     if ((long long)c->Lx * c->Ly * 4 >= (1ll << 31))
         return fail(SQ_E_ARG, "plane exceeds 2 GiB (32-bit buffer offsets)");
     if (c->Lz >= (1ll << 31)) return fail(SQ_E_ARG, "Lz must be < 2^31 (32-bit plane indices)");
+    {   // the guard's fast path (Phi4StepArgs::fin) needs every update of a field
+        // inside [-clamp, clamp] to be finite or +-inf, never NaN: bound the drift
+        const double cl = p.clamp, h = p.deltatau;
+        const double drift = 12.0 * cl + std::fabs(p.m2) * cl + std::fabs(p.lambda) / 6.0 * cl * cl * cl;
+        if (!std::isfinite(cl) || !(cl > 0) || !std::isfinite(p.m2) || !std::isfinite(p.lambda) ||
+            !std::isfinite(p.C) || !(h * drift + cl + 16.0 * sqrt(2.0 * h) * std::fabs(p.C) < 1e30))
+            return fail(SQ_E_ARG, "PHI4 parameters must be finite with dtau * drift(clamp) < 1e30");
+    }
     if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
         const int r = atoi(e), rs = 64 / c->geom.qx;
         if ((r == 1 || r == 2 || r == 4) && c->Ly % r == 0)
@@ -733,10 +756,10 @@ int create_phi4(sq_ctx *c) {
     // profiles/r01/fuse2_slabs.log).
     // Rows of several 256-site segments fuse through the x-halo wave: measured
     // (profiles/r02/sweep_tb2_*.log, us per step, fused vs one step per launch)
-    // 1024 x 1024 x 128 194 vs 225, 1024^3 1537 vs 1678, 512^3 197 vs 199 --
-    // a tie at 512-wide rows, which keep the per-step kernel.
+    // 512^3 153 vs 200 (with the guard's fast path; 197 before it), 1024 x
+    // 1024 x 128 194 vs 225, 1024^3 1537 vs 1678.
     const char *fe = getenv("SQ_FUSE2");
-    const bool fuse = fe ? atoi(fe) != 0 : (p.comm != SQ_COMM_LOOPBACK && c->Lx != 512);
+    const bool fuse = fe ? atoi(fe) != 0 : p.comm != SQ_COMM_LOOPBACK;
     if (fuse && sq::phi4_tb2_supported(c->Lx, c->Ly) && (p.comm != SQ_COMM_NONE || c->slabs[0].nz >= 2)) {
         c->tbz = 16;
         if (const char *z = getenv("SQ_FUSE2_Z")) {
@@ -1028,6 +1051,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     if (rc) return rc;
     c->in_frame = true;
     c->frame_step0 = c->step;
+    const bool fin0 = c->field_finite;
     rc = phi4_steps(c, c->p.loops);
     c->in_frame = false;
     if (rc) return rc;
@@ -1068,6 +1092,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     *stable = (h == 0 && c->stab_fired < 0) ? 1 : 0;
     if (!*stable) {  // rollback from the device snapshot; the noise counter is NOT rewound,
                      // so a retried frame draws fresh noise (as the reference's LCG state)
+        c->field_finite = fin0;
         for (auto &s : c->slabs)
             SQ_HIP(hipMemcpyAsync(plane0(c, s, c->cur), s.snap, (size_t)s.nz * plane * sizeof(float),
                                   hipMemcpyDeviceToDevice, s.sA));
@@ -1432,6 +1457,7 @@ int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {
                          hipMemcpyHostToDevice));
         off += (size_t)s.nz * plane;
     }
+    c->field_finite = false;  // the caller's values (NaN / inf / beyond the clamp allowed) meet the full guard
     return SQ_OK;
 }
 
@@ -1463,6 +1489,7 @@ int sq_init_field(sq_ctx *c, float amp) {
     for (auto &s : c->slabs)
         SQ_HIP(sq::phi4_init_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
                                     (uint32_t)(c->p.seed >> 32), amp, s.sA));
+    c->field_finite = std::isfinite(amp) && std::fabs(amp) * 8.0f < (float)c->p.clamp;
     return phi4_join(c);
 }
 
@@ -1502,7 +1529,8 @@ int sq_get_params(sq_ctx *c, sq_params *out) {
 
 int sq_set_dtau(sq_ctx *c, double dtau) {
     if (!c) return fail(SQ_E_ARG, "null context");
-    if (!(dtau > 0)) return fail(SQ_E_ARG, "dtau must be > 0");
+    if (!(dtau > 0) || !std::isfinite(dtau) || (is_phi4(c) && dtau > 1e20))
+        return fail(SQ_E_ARG, "dtau must be finite, > 0 (and <= 1e20 for PHI4: the guard's drift bound)");
     c->dtau = dtau;
     return SQ_OK;
 }

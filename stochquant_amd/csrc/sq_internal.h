@@ -29,6 +29,9 @@ struct Phi4StepArgs {
     long long zg0;            // global z of local plane 0
     long long Lzg;            // global Lz (the noise index of ghost-zone planes wraps)
     float h, m2, lam6, sig, clampv;
+    float sigq;               // sig * sqrt(2 ln 2): the amplitude of the kernels' box_muller_q normals
+    int fin;                  // the input field is known finite (every plane has been through the
+                              // guard): the guard then runs only where |phi'| >= clampv
     uint32_t k0, k1, s_lo, s_hi;
     int *flag;                // guard flag: set to 1 when a site was clamped / NaN (nullable: frames only)
     // stability records of this launch's step(s) (nullable; frames only): for
@@ -39,6 +42,7 @@ struct Phi4StepArgs {
     unsigned int *st_a;
 };
 constexpr int kStabSlots = 32;
+constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2): box_muller_q's missing factor (sq_rng.h)
 
 struct Phi4Geom {
     int qx;   // lanes per x segment (4 sites each)

@@ -90,7 +90,7 @@ __device__ __forceinline__ float site_update(float phi, float xm, float xp, floa
     const float g = __builtin_fmaf(A.lam6, phi * phi, A.m2);
     const float drift = __builtin_fmaf(-phi, g, lap);
     const float det = __builtin_fmaf(A.h, drift, phi);
-    const float v = NZ ? __builtin_fmaf(A.sig, xi, det) : det;  // NZ = false: C = 0 gradient flow
+    const float v = NZ ? __builtin_fmaf(A.sigq, xi, det) : det;  // NZ = false: C = 0 gradient flow
     return fmaxf(fminf(v, A.clampv), -A.clampv);
 }
 
@@ -99,10 +99,15 @@ __device__ __forceinline__ float site_update(float phi, float xm, float xp, floa
 // operations and order per site, so bit-identical results; the x-neighbour
 // sums stay scalar (their operands are not register-pair aligned).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+// fin: the inputs are known finite (Phi4StepArgs::fin) -- then a finite
+// update can only leave [-clampv, clampv] as a finite value or an infinity
+// (create_phi4 bounds the drift), never as NaN, so one max3 / max / compare
+// decides whether the guard has anything to do and the 8-instruction guard
+// runs only in waves where some lane does (bit-identical either way).
 template <bool NZ>
 __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, float4 up, float4 dn,
                                                float4 zm, float4 zp, const f32x4n &xi,
-                                               const Phi4StepArgs &A) {
+                                               const Phi4StepArgs &A, bool fin) {
     const f32x2 c0 = {c.x, c.y}, c1 = {c.z, c.w};
     const f32x2 x0 = {lft + c.y, c.x + c.z}, x1 = {c.y + c.w, c.z + rgt};
     const f32x2 y0 = f32x2{up.x, up.y} + f32x2{dn.x, dn.y}, y1 = f32x2{up.z, up.w} + f32x2{dn.z, dn.w};
@@ -114,13 +119,17 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
     const f32x2 d0 = __builtin_elementwise_fma(-c0, g0, lap0), d1 = __builtin_elementwise_fma(-c1, g1, lap1);
     f32x2 v0 = __builtin_elementwise_fma(h, d0, c0), v1 = __builtin_elementwise_fma(h, d1, c1);
     if (NZ) {
-        const f32x2 sg = {A.sig, A.sig};
+        const f32x2 sg = {A.sigq, A.sigq};
         v0 = __builtin_elementwise_fma(sg, f32x2{xi.a, xi.b}, v0);
         v1 = __builtin_elementwise_fma(sg, f32x2{xi.c, xi.d}, v1);
     }
     const float cl = A.clampv;
-    return make_float4(fmaxf(fminf(v0.x, cl), -cl), fmaxf(fminf(v0.y, cl), -cl), fmaxf(fminf(v1.x, cl), -cl),
-                       fmaxf(fminf(v1.y, cl), -cl));
+    float4 o = make_float4(v0.x, v0.y, v1.x, v1.y);
+    const float m = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)), fabsf(o.w));  // v_max3 + v_max
+    if (!fin || !(m < cl))
+        o = make_float4(fmaxf(fminf(o.x, cl), -cl), fmaxf(fminf(o.y, cl), -cl), fmaxf(fminf(o.z, cl), -cl),
+                        fmaxf(fminf(o.w, cl), -cl));
+    return o;
 }
 
 // Per-lane frame accumulators (frames only, A.flag != nullptr): the guard
@@ -148,7 +157,7 @@ __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, 
     const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
     f.bad |= (int)(m >= A.clampv);
     if (A.st_md != nullptr) {
-        const float s = NZ ? A.sig : 0.f;
+        const float s = NZ ? A.sigq : 0.f;
         stab_site(f, o.x, c.x, xi.a, s);
         stab_site(f, o.y, c.y, xi.b, s);
         stab_site(f, o.z, c.z, xi.c, s);
@@ -282,9 +291,9 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         for (int k = 0; k < R * V; ++k) c[k] = u32x4{qbase + L.qoff[k], kStreamField << 24, slo, shi};
         philox_rows<R * V>(c, A.k0, A.k1);
 #pragma unroll
-        for (int k = 0; k < R * V; ++k) {
-            box_muller(c[k].x, c[k].y, xi[k].a, xi[k].b);
-            box_muller(c[k].z, c[k].w, xi[k].c, xi[k].d);
+        for (int k = 0; k < R * V; ++k) {  // scaled by 1/sqrt(2 ln 2); A.sigq carries the factor
+            box_muller_q(c[k].x, c[k].y, xi[k].a, xi[k].b);
+            box_muller_q(c[k].z, c[k].w, xi[k].c, xi[k].d);
         }
     } else {
 #pragma unroll
@@ -331,7 +340,7 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
             }
             float4 o;
             if constexpr (PK) {
-                o = site_update4<NZ>(cc, lft, rgt, up, dn, P.row[k], N.row[k], xi[k], A);
+                o = site_update4<NZ>(cc, lft, rgt, up, dn, P.row[k], N.row[k], xi[k], A, A.fin != 0);
             } else {
                 o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[k].x, N.row[k].x, xi[k].a, A);
                 o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[k].y, N.row[k].y, xi[k].b, A);
@@ -495,8 +504,8 @@ __device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, int zl, uint32
         u32x4 c[1];
         c[0] = u32x4{(uint32_t)global_z(A, zl) * qplane + qoff, kStreamField << 24, slo, shi};
         philox_rows<1>(c, A.k0, A.k1);
-        box_muller(c[0].x, c[0].y, xi.a, xi.b);
-        box_muller(c[0].z, c[0].w, xi.c, xi.d);
+        box_muller_q(c[0].x, c[0].y, xi.a, xi.b);  // scaled by 1/sqrt(2 ln 2); A.sigq carries the factor
+        box_muller_q(c[0].z, c[0].w, xi.c, xi.d);
     } else {
         xi = f32x4n{0.f, 0.f, 0.f, 0.f};
     }
@@ -531,7 +540,7 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
     const float g = __builtin_fmaf(A.lam6, phi * phi, A.m2);
     const float drift = __builtin_fmaf(-phi, g, lap);
     const float det = __builtin_fmaf(A.h, drift, phi);
-    const float v = nz ? __builtin_fmaf(A.sig, xi, det) : det;
+    const float v = nz ? __builtin_fmaf(A.sigq, xi, det) : det;
     return fmaxf(fminf(v, A.clampv), -A.clampv);
 }
 
@@ -560,7 +569,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             if (K.lane == 0) lft = ex;
             if (K.lane == 63) rgt = ex;
         }
-        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A);
+        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0);
         if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa);
         const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
         lds[sl][K.w][K.lane] = T2;
@@ -584,7 +593,8 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             if (K.lane == 0) lft = tx[sp][K.w][0];
             if (K.lane == 63) rgt = tx[sp][K.w][1];
         }
-        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A);
+        // step s+1 reads step s's guarded output: always finite
+        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true);
         if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb);
         const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
         bstore4<17>(ws, K.voff, o);
