@@ -60,7 +60,29 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU sample")
     ap.add_argument("--no-profile-events", action="store_true",
                     help="no hipEvents in the timed region (roofline.achieved then uses wall time)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="set up the ranks and their process group, print each rank's slab and deep-halo "
+                         "schedule, touch no GPU (tests the multi-rank launch path on a CPU host)")
     return ap.parse_args()
+
+
+def dry_run(a, world, rank, local, dist):
+    """The multi-rank set-up without a device: every rank reports its slab, its
+    device ordinal and the first block's schedule; rank 0 prints them."""
+    from stochquant_amd.decomp import block_plan, slab_bounds
+    L = a.size
+    Lz = L if a.strong else L * world
+    z0, z1 = slab_bounds(Lz, world, rank)
+    g = max(1, min(16, (z1 - z0) // 16))
+    info = {"rank": rank, "local_rank": local, "world": world, "slab": [z0, z1], "ghost": g,
+            "plan": [o["op"] for o in block_plan(z1 - z0, g, g)] if world > 1 else None}
+    allinfo = [None] * world
+    if world > 1:
+        dist.all_gather_object(allinfo, info)
+    else:
+        allinfo = [info]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": allinfo}), flush=True)
 
 
 def _free_port():
@@ -73,7 +95,9 @@ def _free_port():
 
 def spawn_ranks(n):
     """Start n rank processes of this script (no GPU call has been made here),
-    relay rank 0's stdout, return the worst exit code."""
+    relay rank 0's stdout, return the worst exit code.  A rank that fails ends
+    the others (they would otherwise wait in the rendezvous or a collective)."""
+    import threading
     port = str(_free_port())
     procs = []
     for r in range(n):
@@ -81,15 +105,19 @@ def spawn_ranks(n):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out = procs[0].stdout.read().decode()
-    rcs = []
-    for p in procs:
-        rcs.append(p.wait())
-    if any(rcs):  # a failed rank: make sure none is left behind
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
-    sys.stdout.write(out)
+    out = []
+    reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read().decode()), daemon=True)
+    reader.start()
+    while any(p.poll() is None for p in procs):
+        if any(p.poll() not in (None, 0) for p in procs):
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
+    rcs = [p.wait() for p in procs]
+    reader.join(timeout=10)
+    sys.stdout.write("".join(out))
     sys.stdout.flush()
     return max(rcs, key=abs)
 
@@ -173,6 +201,11 @@ def main():
         # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.dry_run:
+        dry_run(a, world, rank, local, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     torch.cuda.set_device(local)
     L = a.size
     shape = (L, L, L) if a.strong else (L, L, L * world)

@@ -1,0 +1,47 @@
+"""bench.py's launch paths on a CPU host (--dry-run: ranks, process group and
+schedule, no device): run bare with --gpus N it spawns its N rank processes
+itself (the driver's scaling runs need no torchrun), under a launcher
+(RANK / WORLD_SIZE set) it is one rank; rank 0 relays the single JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _run(args, env=None, timeout=180):
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_bench_spawns_its_ranks(n):
+    d = _run(["--gpus", str(n), "--dry-run"])
+    assert d["dry_run"] and d["n_gpus"] == n
+    ranks = sorted(d["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == list(range(n)) and [r["local_rank"] for r in ranks] == list(range(n))
+    # weak scaling: 256^3 per rank, contiguous slabs covering 256 n planes
+    assert [r["slab"] for r in ranks] == [[256 * k, 256 * (k + 1)] for k in range(n)]
+    assert all(r["plan"][0] == "exchange" and "pair" in r["plan"] for r in ranks)
+
+
+def test_bench_strong_split():
+    d = _run(["--gpus", "2", "--dry-run", "--strong", "--size", "64"])
+    assert [r["slab"] for r in sorted(d["ranks"], key=lambda r: r["rank"])] == [[0, 32], [32, 64]]
+
+
+def test_bench_single_rank_under_a_launcher():
+    """RANK / WORLD_SIZE present (torch.distributed.run): no spawning."""
+    d = _run(["--dry-run"], env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
+    assert d["n_gpus"] == 1 and d["ranks"][0]["plan"] is None
