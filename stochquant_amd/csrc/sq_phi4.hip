@@ -206,6 +206,67 @@ __device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAc
     }
 }
 
+// Philox4x32-10 of the field-noise counters {q, cy, cz, cw} whose words 1..3
+// (stream, step lo, step hi) and key are wave-uniform, R independent q per
+// lane, round-major so the chains interleave.  The same function as
+// philox4x32_10 (sq_rng.h), with the first three rounds written out so every
+// combination of uniform words happens on the scalar unit: round 0's
+// M1 * cz product and its xor with cy, k0 (and cw ^ k1), round 1's M0 * n0
+// product, round 2's n3 ^ k1 -- VOP3 reads one scalar per instruction on
+// gfx950, so a v_bitop3_b32 of two uniform operands otherwise costs a
+// v_mov_b32 first.  Rounds 3..9: the three-input xors are one v_bitop3_b32 each.
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+template <int R>
+__device__ __forceinline__ void philox_field(u32x4 (&c)[R], uint32_t k0, uint32_t k1) {
+    const uint32_t cy = uni(c[0].y), cz = uni(c[0].z), cw = uni(c[0].w);
+    // round 0
+    const uint64_t p1u = (uint64_t)kPhiloxM1 * cz;
+    const uint32_t u0 = uni((uint32_t)(p1u >> 32) ^ cy ^ k0), u1 = uni((uint32_t)p1u);
+    const uint32_t a0 = uni(cw ^ k1);
+    uint32_t n2[R], n3[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c[r].x;
+        n2[r] = (uint32_t)(p0 >> 32) ^ a0;
+        n3[r] = (uint32_t)p0;
+    }
+    // round 1
+    k0 += kPhiloxW0;
+    k1 += kPhiloxW1;
+    const uint64_t p0u = (uint64_t)kPhiloxM0 * u0;
+    const uint32_t b0 = uni(u1 ^ k0), b2 = uni((uint32_t)(p0u >> 32) ^ k1), u3 = uni((uint32_t)p0u);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t p1 = (uint64_t)kPhiloxM1 * n2[r];
+        c[r] = u32x4{(uint32_t)(p1 >> 32) ^ b0, (uint32_t)p1, b2 ^ n3[r], u3};
+    }
+    // round 2: word 3 is still uniform
+    k0 += kPhiloxW0;
+    k1 += kPhiloxW1;
+    const uint32_t d2 = uni(u3 ^ k1);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint64_t p0 = (uint64_t)kPhiloxM0 * c[r].x;
+        const uint64_t p1 = (uint64_t)kPhiloxM1 * c[r].z;
+        const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c[r].y, k0, 0x96);
+        c[r] = u32x4{n0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ d2, (uint32_t)p0};
+    }
+#pragma unroll
+    for (int rnd = 3; rnd < 10; ++rnd) {
+        k0 += kPhiloxW0;
+        k1 += kPhiloxW1;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint64_t p0 = (uint64_t)kPhiloxM0 * c[r].x;
+            const uint64_t p1 = (uint64_t)kPhiloxM1 * c[r].z;
+            const uint32_t n0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p1 >> 32), c[r].y, k0, 0x96);
+            const uint32_t m2 = __builtin_amdgcn_bitop3_b32((uint32_t)(p0 >> 32), c[r].w, k1, 0x96);
+            c[r] = u32x4{n0, (uint32_t)p1, m2, (uint32_t)p0};
+        }
+    }
+}
+
 // Philox4x32-10 on R independent counters, round-major so the R dependency
 // chains interleave; the three-input xors are one v_bitop3_b32 each.
 template <int R>
@@ -289,7 +350,7 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
         const uint32_t qbase = (uint32_t)global_z(A, z) * qplane;
 #pragma unroll
         for (int k = 0; k < R * V; ++k) c[k] = u32x4{qbase + L.qoff[k], kStreamField << 24, slo, shi};
-        philox_rows<R * V>(c, A.k0, A.k1);
+        philox_field<R * V>(c, A.k0, A.k1);
 #pragma unroll
         for (int k = 0; k < R * V; ++k) {  // scaled by 1/sqrt(2 ln 2); A.sigq carries the factor
             box_muller_q(c[k].x, c[k].y, xi[k].a, xi[k].b);
@@ -503,7 +564,7 @@ __device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, int zl, uint32
     if constexpr (NZ) {
         u32x4 c[1];
         c[0] = u32x4{(uint32_t)global_z(A, zl) * qplane + qoff, kStreamField << 24, slo, shi};
-        philox_rows<1>(c, A.k0, A.k1);
+        philox_field<1>(c, A.k0, A.k1);
         box_muller_q(c[0].x, c[0].y, xi.a, xi.b);  // scaled by 1/sqrt(2 ln 2); A.sigq carries the factor
         box_muller_q(c[0].z, c[0].w, xi.c, xi.d);
     } else {
