@@ -228,7 +228,9 @@ def main():
             dist.barrier()
 
     if slab_path:
-        lat.step(84)   # setup: the ghost-depth trial blocks (3 x (4 + 8 + 16) steps) when autotuning
+        # setup: the timed trial blocks of the multi-rank slab path, 3 x G steps per
+        # candidate (G, core pairs) in {(4,1), (8,1), (16,1), (16,2), (16,4)}
+        lat.step(180)
     # clock settle: untimed batches until settle_ms have passed on rank 0 (every
     # rank runs the same batches: the slab exchanges must pair up)
     settle_steps = 0

@@ -89,6 +89,8 @@ typedef struct sq_perf_t {
                                   [lo-2, hi+2) of the latest field */
 #define SQ_OP_WAIT_EXCHANGE 3  /* stream A waits for this block's exchange */
 #define SQ_OP_EDGES_DONE 4     /* stream A: the planes the next exchange sends are final (event) */
+#define SQ_OP_WAIT_STAGED 5    /* stream A waits until the exchange has copied its edge planes aside (an
+                                  EXCHANGE op with lo = 1 sends from that staged copy) */
 typedef struct sq_block_op {
     int kind;                  /* SQ_OP_* */
     int step;                  /* block-relative index of the (first) step computed */
@@ -166,13 +168,14 @@ int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
 /* The launch schedule of one deep-halo block (pure host logic, no device
  * needed; the product's phi4_block executes exactly this list): a slab of nz
  * planes with a ghost zone of `ghost` planes (the exchange depth G) running
- * g <= G steps; fuse2 != 0 runs the inner steps as two-step pairs, edge_first
+ * g <= G steps; fuse2 != 0 runs the steps as two-step pairs, the first
+ * core_pairs of them on the ghost-free core ahead of the exchange; edge_first
  * != 0 computes the last step's edge planes first.  Writes *nops ops (at most
  * cap).  sq_phi4_pick_ghost returns the index of the fastest candidate of the
  * rank-max-reduced per-step times ms[n] (the ghost-depth trial, identical on
  * every rank once the times are reduced). */
-int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
-                       int *nops);
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, sq_block_op *ops,
+                       int cap, int *nops);
 int sq_phi4_pick_ghost(const double *ms, int n);
 /* PHI4 frame stability (the heuristic of tau_kernel.cl:135-143 restated for
  * the 3-D lattice).  Every frame records per step j the maximum

@@ -67,6 +67,8 @@ struct Slab {
     hipStream_t sA = nullptr, sB = nullptr;
     hipEvent_t evA = nullptr, evC = nullptr;  // A: block's steps done; C: its halo exchange done
     hipEvent_t evE = nullptr;                 // E: the block's output edge planes (what the next exchange sends) done
+    float *stage = nullptr;                   // 2 G planes: the staged copy of the edge planes an exchange sends
+    hipEvent_t evS = nullptr;                 // S: the staged copy is complete (the field's edges may change)
 };
 
 struct EvPair {
@@ -132,6 +134,7 @@ struct sq_ctx {
     int gz = 1;    // active ghost-zone depth (planes) of slab decompositions = steps per halo exchange
     int gpad = 1;  // allocated ghost planes on either side of each slab (gz <= gpad)
     bool g_auto = false, g_tuned = false;  // ghost depth chosen by timed trial blocks (phi4_autotune)
+    bool k_auto = true;                    // ... and the core pairs (unless SQ_CORE_PAIRS pins them)
     double *dtune = nullptr;
     std::vector<Slab> slabs;
     int cur = 0;
@@ -140,6 +143,8 @@ struct sq_ctx {
     bool field_finite = true;  // every plane of the current field has been through the guard (or
                                // came from sq_init_field); false after a caller's upload / load
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
+    int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange
+                            // (SQ_CORE_PAIRS pins; multi-rank runs time 1, 2, 4 on the real link)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;  // [0] max |phi| bits, [1] ordered max phi
     // stability heuristic of phi4 frames (tau_kernel.cl:135-143):
@@ -354,18 +359,28 @@ int phi4_periodic_step(sq_ctx *c) {
 //                of the block's input field to both z-neighbours, their ghosts in;
 //   then stream A.  Step k updates the shrinking extended range
 //   [-(g-1-k), nz+g-1-k), recomputing ghost-zone sites.  With fuse2 (two steps
-//   per launch) and g >= 3 every step runs in pairs:
-//     PAIR 0 core   step 1 on [2, nz-2): reads only [0, nz), so it overlaps the exchange;
-//     WAIT_EXCHANGE, PAIR 0 rim: step 1 on [-(g-2), 2) u [nz-2, nz+g-2) (one launch);
-//     PAIR s        steps s, s+1 on step s+1's range, reading step s-1's;
+//   per launch) and g >= 3 every step runs in pairs, and the first K pairs
+//   (kc = core pairs) are split around the exchange:
+//     PAIR 2j core  step 2j+1 on [2j+2, nz-2j-2), j < K: reads no ghost (step s
+//                   is valid without ghosts on [s+1, nz-s-1)), so all K of them
+//                   overlap the exchange;
+//     WAIT_EXCHANGE;
+//     PAIR 2j rim   step 2j+1 on [-(g-2-2j), 2j+2) u [nz-2j-2, nz+g-2-2j), j < K
+//                   (two ranges of g planes, one launch);
+//     PAIR s        the remaining pairs on step s+1's whole range, reading step s-1's;
 //     the last pair (or single step) computes its edge planes [0, G) u
 //     [nz-G, nz) first and marks EDGES_DONE, so the NEXT block's exchange
-//     overlaps this step's middle as well as the next core;
+//     overlaps this step's middle as well as the next cores (when the core
+//     pairs reach the last step, its middle is done before the exchange and
+//     EDGES_DONE follows the last rims);
 //   without fuse2 (or g < 3) step 0 is a single-step core [1, nz-1) / rim
 //   [-(g-1), 1) u [nz-1, nz+g-1) split and the later steps single launches.
 // Ghost-zone sites are recomputed redundantly; the counter-based noise makes
 // them bit-identical to their owner's, so the result equals the monolithic run.
-std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first) {
+// Buffers: pair j writes step 2j+1 into the other buffer of step 2j-1's; a
+// core pair running ahead of the rims only writes [2j+2, nz-2j-2), which no
+// earlier rim pair reads ([.., 2i+4) u [nz-2i-4, ..) for i < j).
+std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first, int kc) {
     std::vector<sq_block_op> ops;
     auto add = [&](int kind, int step, int lo, int hi, int lo2 = 0, int hi2 = 0) {
         ops.push_back(sq_block_op{kind, step, lo, hi, lo2, hi2});
@@ -373,15 +388,29 @@ std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_
     const bool split_edges = edge_first && nz > 2 * G;
     add(SQ_OP_EXCHANGE, 0, 0, 0);
     int st;
+    bool edges = false;
     if (fuse2 && g >= 3) {
-        if (nz > 4) add(SQ_OP_PAIR, 0, 2, nz - 2);
+        // core pairs: at least one, at most the pairs of the block, and only
+        // while the core is not empty
+        int K = std::max(1, std::min(kc, g / 2));
+        while (K > 1 && nz <= 4 * K) --K;
+        // core pair 1 writes step 3 into the buffer the exchange sends its edge
+        // planes from: with K >= 2 the exchange sends a staged copy of them, and
+        // core pair 1 waits only for that copy
+        if (K >= 2) ops[0].lo = 1;
+        for (int j = 0; j < K && nz > 4 * j + 4; ++j) {
+            if (j == 1) add(SQ_OP_WAIT_STAGED, 0, 0, 0);
+            add(SQ_OP_PAIR, 2 * j, 2 * j + 2, nz - 2 * j - 2);
+        }
         add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
-        const int lo_a = -(g - 2), hi_a = 2, lo_b = nz - 2, hi_b = nz + g - 2;
-        if (hi_a >= lo_b)  // rims meet (nz <= 4): one span
-            add(SQ_OP_PAIR, 0, lo_a, hi_b);
-        else
-            add(SQ_OP_PAIR, 0, lo_a, hi_a, lo_b, hi_b);
-        st = 2;
+        for (int j = 0; j < K; ++j) {
+            const int lo_a = -(g - 2 - 2 * j), hi_a = 2 * j + 2, lo_b = nz - 2 * j - 2, hi_b = nz + g - 2 - 2 * j;
+            if (hi_a >= lo_b)  // rims meet (no core): one span
+                add(SQ_OP_PAIR, 2 * j, lo_a, hi_b);
+            else
+                add(SQ_OP_PAIR, 2 * j, lo_a, hi_a, lo_b, hi_b);
+        }
+        st = 2 * K;
     } else {
         if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1);
         add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
@@ -392,7 +421,6 @@ std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_
             add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b);
         st = 1;
     }
-    bool edges = false;
     while (st < g) {
         const bool pair = fuse2 && st + 1 <= g - 1;
         const int last = pair ? st + 1 : st;  // the step this op group completes
@@ -419,7 +447,18 @@ int phi4_block(sq_ctx *c, int g) {
     const size_t gbytes = (size_t)G * plane * sizeof(float);
     const int cur = c->cur;
     const unsigned long long step0 = c->step;
-    // 1. exchange (stream B), for every slab before any slab waits for one
+    std::vector<std::vector<sq_block_op>> plans;
+    for (const Slab &s : c->slabs) plans.push_back(block_plan(s.nz, G, g, c->tbz > 0, c->edge_first, c->core_pairs));
+    // 1. exchange (stream B), for every slab before any slab waits for one;
+    //    staged (EXCHANGE op lo = 1): the edge planes are copied aside first and
+    //    sent from the copy, so the block's core pairs may overwrite them early
+    std::vector<const float *> src_lo(ns), src_hi(ns);
+    for (int i = 0; i < ns; ++i) {
+        Slab &s = c->slabs[i];
+        const float *p0 = plane0(c, s, cur);
+        src_lo[i] = p0;
+        src_hi[i] = p0 + (size_t)(s.nz - G) * plane;
+    }
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
         SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
@@ -428,17 +467,26 @@ int phi4_block(sq_ctx *c, int g) {
             SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evE, 0));
         }
     }
+    for (int i = 0; i < ns; ++i) {
+        Slab &s = c->slabs[i];
+        if (plans[i][0].lo != 1) continue;
+        if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
+        SQ_HIP(hipMemcpyAsync(s.stage, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(hipMemcpyAsync(s.stage + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(hipEventRecord(s.evS, s.sB));
+        src_lo[i] = s.stage;
+        src_hi[i] = s.stage + (size_t)G * plane;
+    }
     if (c->p.comm == SQ_COMM_LOOPBACK) {
         for (int i = 0; i < ns; ++i) {
             Slab &s = c->slabs[i];
             Slab &dn = c->slabs[(i + ns - 1) % ns];
             Slab &up = c->slabs[(i + 1) % ns];
-            const float *p0 = plane0(c, s, cur);
             // my bottom G planes -> lower neighbour's upper ghosts [nz_dn, nz_dn+G)
-            SQ_HIP(hipMemcpyAsync(plane0(c, dn, cur) + (size_t)dn.nz * plane, p0, gbytes,
+            SQ_HIP(hipMemcpyAsync(plane0(c, dn, cur) + (size_t)dn.nz * plane, src_lo[i], gbytes,
                                   hipMemcpyDeviceToDevice, s.sB));
             // my top G planes -> upper neighbour's lower ghosts [-G, 0)
-            SQ_HIP(hipMemcpyAsync(plane0(c, up, cur) - (size_t)G * plane, p0 + (size_t)(s.nz - G) * plane, gbytes,
+            SQ_HIP(hipMemcpyAsync(plane0(c, up, cur) - (size_t)G * plane, src_hi[i], gbytes,
                                   hipMemcpyDeviceToDevice, s.sB));
             SQ_HIP(hipEventRecord(s.evC, s.sB));
             c->perf.halo_bytes += 2.0 * (double)gbytes;
@@ -450,8 +498,8 @@ int phi4_block(sq_ctx *c, int g) {
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
         const size_t n = (size_t)G * plane;
         SQ_NCCL(ncclGroupStart());
-        SQ_NCCL(ncclSend(p0 + (size_t)(s.nz - G) * plane, n, ncclFloat32, up, c->comm, s.sB));
-        SQ_NCCL(ncclSend(p0, n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCL(ncclSend(src_hi[0], n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCL(ncclSend(src_lo[0], n, ncclFloat32, dn, c->comm, s.sB));
         SQ_NCCL(ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, s.sB));
         SQ_NCCL(ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
         SQ_NCCL(ncclGroupEnd());
@@ -463,7 +511,7 @@ int phi4_block(sq_ctx *c, int g) {
     int out_buf = cur;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        const std::vector<sq_block_op> ops = block_plan(s.nz, G, g, c->tbz > 0, c->edge_first);
+        const std::vector<sq_block_op> &ops = plans[i];
         int in = cur;            // buffer holding the latest completed step
         bool flip = false;       // the current op group writes in ^ 1
         int gstep = -1, gkind = -1;  // the current op group: ops of one kind and step read the same buffer
@@ -490,6 +538,8 @@ int phi4_block(sq_ctx *c, int g) {
                     SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
                     SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
                 }
+            } else if (op.kind == SQ_OP_WAIT_STAGED) {
+                SQ_HIP(hipStreamWaitEvent(s.sA, s.evS, 0));
             } else if (op.kind == SQ_OP_EDGES_DONE) {
                 SQ_HIP(hipEventRecord(s.evE, s.sA));
             } else if (op.kind != SQ_OP_EXCHANGE) {  // the exchange was issued above for every slab
@@ -515,20 +565,29 @@ int phi4_join(sq_ctx *c);
 // every rank picks the same G (exchange sizes must match).  The trial steps
 // are ordinary steps: the field is the same for any G.
 int phi4_autotune(sq_ctx *c, int &n) {
-    std::vector<int> cand;
+    struct Cand {
+        int g, k;
+    };
+    std::vector<Cand> cand;
     for (int g : {4, 8, 16})
-        if (g <= c->gpad) cand.push_back(g);
-    if (cand.empty()) cand.push_back(c->gpad);
+        if (g <= c->gpad) cand.push_back({g, c->core_pairs});
+    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs});
+    // with fused pairs, how many core pairs run ahead of the exchange: the
+    // deepest ghost zone's block tried with 2 and 4 as well
+    if (c->tbz > 0 && c->k_auto)
+        for (int k : {2, 4})
+            if (k <= cand.back().g / 2) cand.push_back({cand.back().g, k});
     int need = 0;
-    for (int g : cand) need += 3 * g;
+    for (const Cand &k : cand) need += 3 * k.g;
     if (n < need) return SQ_OK;  // too few steps requested: try again on a later call
     hipEvent_t t0, t1;
     SQ_HIP(hipEventCreate(&t0));
     SQ_HIP(hipEventCreate(&t1));
     std::vector<double> ms(cand.size());
     for (size_t k = 0; k < cand.size(); ++k) {
-        const int g = cand[k];
+        const int g = cand[k].g;
         c->gz = g;
+        c->core_pairs = cand[k].k;
         int rc = phi4_block(c, g);
         if (!rc) rc = phi4_join(c);
         if (rc) return rc;
@@ -553,7 +612,9 @@ int phi4_autotune(sq_ctx *c, int &n) {
         SQ_HIP(hipMemcpyAsync(ms.data(), c->dtune, sizeof(double) * ms.size(), hipMemcpyDeviceToHost, st));
         SQ_HIP(hipStreamSynchronize(st));
     }
-    c->gz = cand[(size_t)sq_phi4_pick_ghost(ms.data(), (int)ms.size())];
+    const Cand best = cand[(size_t)sq_phi4_pick_ghost(ms.data(), (int)ms.size())];
+    c->gz = best.g;
+    c->core_pairs = best.k;
     c->g_tuned = true;
     return SQ_OK;
 }
@@ -710,6 +771,8 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipEventCreateWithFlags(&s.evA, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evC, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evE, hipEventDisableTiming));
+        SQ_HIP(hipEventCreateWithFlags(&s.evS, hipEventDisableTiming));
+        if (p.comm != SQ_COMM_NONE) SQ_HIP(hipMalloc(&s.stage, 2 * (size_t)c->gpad * plane * sizeof(float)));
         SQ_HIP(hipEventRecord(s.evA, s.sA));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         SQ_HIP(hipEventRecord(s.evE, s.sA));
@@ -742,6 +805,10 @@ int create_phi4(sq_ctx *c) {
     while (zc < 32 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 32768) zc *= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
+    if (const char *e = getenv("SQ_CORE_PAIRS")) {
+        c->core_pairs = std::max(1, atoi(e));
+        c->k_auto = false;
+    }
     c->zc = zc;
     // Two steps per launch on 256-wide lattices (SQ_FUSE2=0: off; SQ_FUSE2_Z:
     // pin the output planes per block), single slab and deep-halo slabs alike.
@@ -1183,6 +1250,8 @@ int sq_destroy(sq_ctx *c) {
         if (s.evA) (void)hipEventDestroy(s.evA);
         if (s.evC) (void)hipEventDestroy(s.evC);
         if (s.evE) (void)hipEventDestroy(s.evE);
+        if (s.evS) (void)hipEventDestroy(s.evS);
+        (void)hipFree(s.stage);
     }
     for (int k = 0; k < 2; ++k) {
         (void)hipFree(c->qf[k]);
@@ -1424,11 +1493,11 @@ int sq_phi4_set_stability(sq_ctx *c, double T, double V) {
     return SQ_OK;
 }
 
-int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, sq_block_op *ops, int cap,
-                       int *nops) {
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, sq_block_op *ops,
+                       int cap, int *nops) {
     if (!nops || (cap > 0 && !ops)) return fail(SQ_E_ARG, "null argument");
     if (nz < 1 || ghost < 1 || g < 1 || g > ghost || ghost > nz) return fail(SQ_E_ARG, "need 1 <= g <= ghost <= nz");
-    const std::vector<sq_block_op> v = block_plan(nz, ghost, g, fuse2 != 0, edge_first != 0);
+    const std::vector<sq_block_op> v = block_plan(nz, ghost, g, fuse2 != 0, edge_first != 0, core_pairs);
     *nops = (int)v.size();
     if ((int)v.size() > cap) return fail(SQ_E_ARG, "cap too small: need " + std::to_string(v.size()));
     std::copy(v.begin(), v.end(), ops);

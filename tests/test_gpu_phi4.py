@@ -381,6 +381,29 @@ def test_fused_two_step_deep_halo_bitwise(gpu, oracle_mod, monkeypatch, shape, g
         assert np.array_equal(mono, L.download())
 
 
+@pytest.mark.parametrize("core_pairs", ["2", "4", "8"])
+def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs):
+    """K fused core pairs before the exchange wait, their rims after it (the
+    C4 overlap for slow links): RCCL self-exchange and loopback slabs ==
+    the single-slab run, bit for bit, over full and partial blocks."""
+    from stochquant_amd import unique_id
+    shape = (256, 16, 96)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(37)
+        mono = L.download()
+    monkeypatch.setenv("SQ_CORE_PAIRS", core_pairs)
+    monkeypatch.setenv("SQ_GHOST", "16")
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    for kw in (dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id()), dict(comm="loopback", nslabs=2)):
+        with _lat(shape, **kw) as L:
+            L.upload(phi0)
+            for n in (16, 21):
+                L.step(n)
+            assert np.array_equal(L.download(), mono), kw["comm"]
+
+
 def test_fused_two_step_rccl_frames(gpu, oracle_mod, monkeypatch):
     """RCCL self-exchange slab with fused inner steps, run as frames."""
     from stochquant_amd import unique_id
@@ -506,13 +529,14 @@ def test_slice_correlator_across_slabs(gpu, oracle_mod):
 
 @pytest.mark.parametrize("comm", ["loopback", "rccl"])
 def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
-    """Timed trial blocks pick G in {4, 8, 16}; the trial steps are ordinary
-    steps, so the field after them equals the single-slab run bit for bit."""
+    """Timed trial blocks pick G in {4, 8, 16} and the core pairs that run
+    ahead of the exchange in {1, 2, 4}; the trial steps are ordinary steps, so
+    the field after them equals the single-slab run bit for bit."""
     from stochquant_amd import unique_id
     monkeypatch.setenv("SQ_GHOST_AUTO", "1")
     shape = (256, 8, 128)
     phi0 = _init(oracle_mod, shape)
-    steps = 100            # >= 3*(4+8+16) = 84 trial steps, then 16 more
+    steps = 200            # >= 3*(4+8+16+16+16) = 180 trial steps, then 20 more
     with _lat(shape) as L:
         L.upload(phi0)
         L.step(steps)

@@ -92,11 +92,11 @@ def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn):
                     oracle.phi4_step_range(p, bufs[inb], mid, G, lo - 1, hi + 1, z0, s)
                     oracle.phi4_step_range(p, mid, bufs[inb ^ 1], G, lo, hi, z0, s + 1)
         else:
-            assert k in ("wait_exchange", "edges_done")
+            assert k in ("wait_exchange", "edges_done", "wait_staged")
     return inb ^ 1 if flip else inb
 
 
-def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q):
+def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q, core_pairs=1):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
@@ -127,7 +127,7 @@ def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q):
         cur, done = 0, 0
         while done < steps:
             g = min(G, steps - done)
-            plan = block_plan(nz, G, g, fuse2, edge_first)
+            plan = block_plan(nz, G, g, fuse2, edge_first, core_pairs)
             cur = _run_block(oracle, p, plan, bufs, cur, nz, G, z0, done, world, up, dn)
             done += g
         gathered = [None for _ in range(world)]
@@ -148,21 +148,24 @@ def _monolithic(steps):
     return phi
 
 
-@pytest.mark.parametrize("world,steps,fuse2,edge_first,gpad", [
-    (2, 11, True, True, 4),    # P = 2: both neighbours the same peer; partial last block (11 = 4+4+3)
-    (3, 11, True, True, 4),
-    (2, 9, False, True, 4),    # per-step inner launches
-    (3, 8, True, False, 4),    # edges not first
-    (2, 9, True, True, 8),     # deeper zone: pairs over 2 ghost planes
-    (2, 12, True, True, 2),    # G = 2: blocks of one core/rim step and one edges-first step
-    (3, 10, True, True, 8),    # G = 8 over slabs of 12 planes: rims of 8 planes, no edge split
-    (1, 7, True, True, 4),     # single rank, self-exchange
+@pytest.mark.parametrize("world,steps,fuse2,edge_first,gpad,core_pairs", [
+    (2, 11, True, True, 4, 1),    # P = 2: both neighbours the same peer; partial last block (11 = 4+4+3)
+    (3, 11, True, True, 4, 1),
+    (2, 9, False, True, 4, 1),    # per-step inner launches
+    (3, 8, True, False, 4, 1),    # edges not first
+    (2, 9, True, True, 8, 1),     # deeper zone: pairs over 2 ghost planes
+    (2, 12, True, True, 2, 1),    # G = 2: blocks of one core/rim step and one edges-first step
+    (3, 10, True, True, 8, 1),    # G = 8 over slabs of 12 planes: rims of 8 planes, no edge split
+    (1, 7, True, True, 4, 1),     # single rank, self-exchange
+    (2, 17, True, True, 8, 2),    # two core pairs ahead of the exchange
+    (2, 19, True, True, 8, 4),    # every pair of the block split into core and rim
+    (3, 11, True, False, 8, 3),   # three core pairs, slabs of 12 planes (the core shrinks to 4)
 ])
-def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, oracle_mod):
+def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, core_pairs, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, fuse2, edge_first, gpad, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, fuse2, edge_first, gpad, q, core_pairs))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -197,6 +200,17 @@ def test_block_plan_shapes():
         ("exchange", 0, 0, 0, 0, 0), ("pair", 0, 2, 38, 0, 0), ("wait_exchange", 0, 0, 0, 0, 0),
         ("pair", 0, -1, 2, 38, 41), ("step", 2, 0, 4, 36, 40), ("edges_done", 2, 0, 0, 0, 0),
         ("step", 2, 4, 36, 0, 0)]
+    # K core pairs run ahead of the exchange; their rims follow it, then the rest
+    ops = block_plan(64, 8, 8, core_pairs=2)
+    assert [(o["op"], o["step"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in ops] == [
+        ("exchange", 0, 1, 0, 0, 0), ("pair", 0, 2, 62, 0, 0), ("wait_staged", 0, 0, 0, 0, 0),
+        ("pair", 2, 4, 60, 0, 0),
+        ("wait_exchange", 0, 0, 0, 0, 0), ("pair", 0, -6, 2, 62, 70), ("pair", 2, -4, 4, 60, 68),
+        ("pair", 4, -2, 66, 0, 0), ("pair", 6, 0, 8, 56, 64), ("edges_done", 6, 0, 0, 0, 0),
+        ("pair", 6, 8, 56, 0, 0)]
+    ops = block_plan(64, 8, 8, core_pairs=4)   # every pair split: the last rims are the edges
+    assert [o["op"] for o in ops].count("pair") == 8 and ops[-1]["op"] == "edges_done"
+    assert (ops[-2]["lo"], ops[-2]["hi"], ops[-2]["lo2"], ops[-2]["hi2"]) == (0, 8, 56, 64)
     # unfused: every step 1..g-1 covered once, the last one ghost-free
     ops = block_plan(12, 4, 3, fuse2=False, edge_first=False)
     steps = [(o["step"], o["lo"], o["hi"]) for o in ops if o["op"] == "step"]
