@@ -49,10 +49,14 @@ def parse():
                     help="untimed steps for at least this long before the warm-up (clock settle)")
     ap.add_argument("--size", type=int, default=256, help="per-GPU lattice edge (default 256 = config C2)")
     ap.add_argument("--dtau", type=float, default=0.01)
-    ap.add_argument("--comm", choices=["auto", "rccl", "loopback"], default="auto",
-                    help="auto: one slab at N=1, RCCL slabs at N>1; rccl/loopback force the slab path "
-                         "at N=1 (RCCL self-exchange / --slabs slabs on one GPU) to exercise it")
+    ap.add_argument("--comm", choices=["auto", "rccl", "p2p", "loopback"], default="auto",
+                    help="auto: one slab at N=1, RCCL slabs at N>1; p2p: peer-pointer halos (IPC, no RCCL) "
+                         "at any N; rccl/p2p/loopback force the slab path at N=1 (self-exchange / --slabs "
+                         "slabs on one GPU) to exercise it")
     ap.add_argument("--slabs", type=int, default=2)
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on GPU 0 (rehearses the multi-process --comm p2p path on a one-GPU box; "
+                         "the ranks then share one device, so the rate is not a scaling figure)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling (config C5): the --size^3 lattice is split over the N GPUs "
                          "instead of --size^3 per GPU")
@@ -190,11 +194,11 @@ def main():
     if a.gpus > 1 and "RANK" not in os.environ:
         sys.exit(spawn_ranks(a.gpus))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     a.gpus = world
     import torch
     import torch.distributed as dist
-    from stochquant_amd import Phi4Lattice, unique_id, _lib
+    from stochquant_amd import Phi4Lattice, connect_p2p, unique_id, _lib
     _lib.load()  # fail loudly if the HIP library is missing
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -210,7 +214,13 @@ def main():
     L = a.size
     shape = (L, L, L) if a.strong else (L, L, L * world)
     kw = dict(dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local)
-    if world > 1:
+    if a.comm == "p2p":
+        lat = Phi4Lattice(shape, comm="p2p", nranks=world, rank=rank, **kw)
+        if world > 1:
+            connect_p2p(lat)
+        else:
+            lat.p2p_connect([lat.p2p_handle()])
+    elif world > 1:
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         lat = Phi4Lattice(shape, comm="rccl", nranks=world, rank=rank, comm_id=obj[0], **kw)
@@ -296,7 +306,8 @@ def main():
         except Exception:
             copy = None
         rec, rec_path = pmc_record(L, world, kname) if not slab_path else (None, None)
-        fused = "tb2" in kname and not slab_path
+        # the fused two-step kernel carries most steps (slab paths: all but the odd tails)
+        fused = "tb2" in kname and perf.get("fused_steps", 0) >= 0.5 * perf["steps"]
         out = {
             "metric": METRIC,
             "value": value,
@@ -321,7 +332,7 @@ def main():
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
                 "ghost_depth": lat.ghost[0] if slab_path else None,
                 "parallelism": "single GPU, one stream" if not slab_path else
-                               f"z-slab x{world} ({a.comm if world == 1 else 'rccl'}), halo exchange on "
+                               f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else 'rccl'}), halo exchange on "
                                f"stream B, interior on stream A",
             },
             "roofline": {

@@ -46,6 +46,10 @@ extern "C" {
 #define SQ_COMM_NONE 0      /* one slab, periodic z handled in-kernel */
 #define SQ_COMM_LOOPBACK 1  /* nslabs slabs on this device, halos by D2D copies */
 #define SQ_COMM_RCCL 2      /* one slab per process, halos by ncclSend/ncclRecv over xGMI */
+#define SQ_COMM_P2P 3       /* one slab per process, halos pulled from the neighbours' memory through
+                               IPC peer pointers (copy engines, no CUs), cross-process ordering by
+                               stream-ordered flag writes/waits; frame collectives through peer
+                               memory too (no RCCL); bootstrap: sq_p2p_handle / sq_p2p_connect */
 
 typedef struct sq_params {
     int struct_size;            /* = sizeof(sq_params) */
@@ -62,7 +66,7 @@ typedef struct sq_params {
     int device;                 /* HIP device ordinal (argv[7] was an OpenCL platform index) */
     int adapt_dtau;             /* 1: reference Δτ controller in sq_run_frame (tauhost.c:523-541) */
     int comm;                   /* SQ_COMM_* */
-    int nranks, rank;           /* SQ_COMM_RCCL: processes, this process' rank */
+    int nranks, rank;           /* SQ_COMM_RCCL / SQ_COMM_P2P: processes, this process' rank */
     int nslabs;                 /* SQ_COMM_LOOPBACK: slabs on this device */
     unsigned char comm_id[128]; /* SQ_COMM_RCCL: ncclUniqueId from sq_comm_unique_id on rank 0 */
 } sq_params;
@@ -230,6 +234,17 @@ int sq_sync(sq_ctx *ctx);
 /* RCCL bootstrap: rank 0 creates the id, the caller distributes it (e.g. via
  * torch.distributed) into sq_params.comm_id of every rank. */
 int sq_comm_unique_id(unsigned char out[128]);
+
+/* SQ_COMM_P2P bootstrap: every rank exports one handle blob (IPC handles of
+ * its staging buffer, mailbox and collective slots, plus its rank and the
+ * lattice it was created for); the caller all-gathers the blobs in rank order
+ * (e.g. torch.distributed.all_gather_object) and passes all of them to
+ * sq_p2p_connect, which validates and maps them.  Steps, frames and the
+ * correlator of a P2P context fail with SQ_E_STATE until connected.  Every
+ * rank must run the same sequence of steps (the exchanges pair up by count). */
+#define SQ_P2P_HANDLE_BYTES 512
+int sq_p2p_handle(sq_ctx *ctx, unsigned char out[SQ_P2P_HANDLE_BYTES]);
+int sq_p2p_connect(sq_ctx *ctx, const unsigned char *handles, int nranks); /* nranks * SQ_P2P_HANDLE_BYTES */
 
 /* Device queries / self-tests used by tests and bench (no reference analogue). */
 int sq_device_count(int *n);

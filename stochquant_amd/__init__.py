@@ -10,10 +10,10 @@ library and raises if it is unavailable (there is no CPU fallback).
 """
 from ._lib import (LIB_PATH, TAUHOST_PATH, StochQuantError, StochQuantUnavailable, device_count,
                    load)
-from .langevin import (Phi4Lattice, Qm1dChain, parse_frame_line, run_tauhost, tauhost_argv,
+from .langevin import (Phi4Lattice, Qm1dChain, connect_p2p, parse_frame_line, run_tauhost, tauhost_argv,
                        unique_id)
 
 __all__ = [
     "LIB_PATH", "TAUHOST_PATH", "StochQuantError", "StochQuantUnavailable", "device_count", "load",
-    "Phi4Lattice", "Qm1dChain", "parse_frame_line", "run_tauhost", "tauhost_argv", "unique_id",
+    "Phi4Lattice", "Qm1dChain", "connect_p2p", "parse_frame_line", "run_tauhost", "tauhost_argv", "unique_id",
 ]

@@ -17,6 +17,8 @@ SQ_MODEL_PHI4 = 1
 SQ_COMM_NONE = 0
 SQ_COMM_LOOPBACK = 1
 SQ_COMM_RCCL = 2
+SQ_COMM_P2P = 3
+SQ_P2P_HANDLE_BYTES = 512
 SQ_ORDER_JACOBI = 0
 SQ_ORDER_SERIAL = 1
 
@@ -132,6 +134,8 @@ SIGNATURES = {
     "sq_perf_reset": (ctypes.c_int, [_P]),
     "sq_sync": (ctypes.c_int, [_P]),
     "sq_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ubyte)]),
+    "sq_p2p_handle": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ubyte)]),
+    "sq_p2p_connect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ubyte), ctypes.c_int]),
     "sq_device_count": (ctypes.c_int, [_I]),
     "sq_selftest_normals": (ctypes.c_int, [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_uint,
                                            ctypes.c_ulonglong, ctypes.c_ulonglong, _F, ctypes.c_size_t]),

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/stochquant.h"
@@ -74,6 +75,34 @@ struct Slab {
 struct EvPair {
     hipEvent_t a, b;
 };
+
+// SQ_COMM_P2P: the words of a rank's mailbox its neighbours
+// and peers write with stream-ordered flag writes; every value is a sequence
+// number that only grows, so a wait is ">= this exchange / collective".
+constexpr int kMbStagedFromDn = 0;  // the lower neighbour's staged edge planes of exchange e are complete
+constexpr int kMbStagedFromUp = 1;  // ... the upper neighbour's
+constexpr int kMbAckFromDn = 2;     // the lower neighbour has finished reading our staged copy of exchange e
+constexpr int kMbAckFromUp = 3;     // ... the upper neighbour
+constexpr int kMbColl = 16;         // + q: rank q's contribution to collective k is in our slot q
+constexpr int kMbWords = 1024;
+constexpr int kP2pMaxRanks = kMbWords - kMbColl;
+constexpr unsigned int kP2pMagic = 0x53513250u;  // "SQ2P"
+
+struct Peer {  // a rank's buffers as this process addresses them
+    float *stage = nullptr;
+    unsigned int *mbox = nullptr;
+    unsigned char *coll = nullptr;
+    bool mapped = false;  // opened through IPC (closed by sq_destroy)
+};
+
+struct P2pBlob {  // sq_p2p_handle's output
+    unsigned int magic, version;
+    int rank, nranks, Lx, Ly, gpad, pad;
+    long long Lz, coll_cap;
+    unsigned long long seed;
+    hipIpcMemHandle_t stage, mbox, coll;
+};
+static_assert(sizeof(P2pBlob) <= SQ_P2P_HANDLE_BYTES, "P2P handle blob");
 
 // Inverse of the kernels' order-preserving float -> uint map (sq_phi4.hip ord_f32).
 float unord_f32(unsigned int o) {
@@ -161,6 +190,14 @@ struct sq_ctx {
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
     long long ev_extra_steps = 0;   // profiling mode 1: steps beyond the first in timed launches
     ncclComm_t comm = nullptr;
+    // SQ_COMM_P2P: mailbox, collective slots (2 parities x nranks x coll_cap
+    // bytes) and every rank's buffers as mapped here (own ones at [rank])
+    unsigned int *mbox = nullptr;
+    unsigned char *coll = nullptr;
+    size_t coll_cap = 0;
+    std::vector<Peer> peers;
+    bool p2p_ready = false;
+    unsigned int xchg_seq = 0, coll_seq = 0;  // exchanges / collectives issued so far
     // profiling: 0 off, 1 per launch (hipExtLaunchKernel dispatch timestamps),
     // 2 one event pair around every sq_step call on the step-kernel stream
     int profiling = 0;
@@ -173,6 +210,52 @@ struct sq_ctx {
 namespace {
 
 bool is_phi4(const sq_ctx *c) { return c->p.model == SQ_MODEL_PHI4; }
+
+// one slab per process, ranks of a job (RCCL or peer pointers)
+bool per_rank(int comm) { return comm == SQ_COMM_RCCL || comm == SQ_COMM_P2P; }
+
+hipError_t wait_seq(hipStream_t s, unsigned int *word, unsigned int seq) {
+    return hipStreamWaitValue32(s, word, seq, hipStreamWaitValueGte, 0xFFFFFFFFu);
+}
+
+// Collective over peer memory: our contribution into slot `rank` of every
+// rank's gather buffer (parity seq & 1), a flag to each, wait for every rank's
+// flag, then fold our buffer's slots in rank order (sq_p2p.hip).  Round k + 2
+// reuses round k's slots: a rank issues it only after every rank's flag of
+// round k + 1, which each rank writes after its fold of round k.
+int p2p_allreduce(sq_ctx *c, void *d, size_t n, sq::P2pRed red, hipStream_t st) {
+    const int P = c->p.nranks, r = c->p.rank;
+    if (!c->p2p_ready) return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
+    const size_t esz = (red == sq::P2pRed::kMaxU32 || red == sq::P2pRed::kMaxI32) ? 4 : 8;
+    if (n * esz > c->coll_cap) return fail(SQ_E_ARG, "collective larger than the P2P slot");
+    const unsigned int seq = ++c->coll_seq;
+    const size_t base = (size_t)(seq & 1u) * (size_t)P * c->coll_cap;
+    for (int q = 0; q < P; ++q)
+        SQ_HIP(hipMemcpyAsync(c->peers[q].coll + base + (size_t)r * c->coll_cap, d, n * esz, hipMemcpyDeviceToDevice, st));
+    for (int q = 0; q < P; ++q) SQ_HIP(hipStreamWriteValue32(st, c->peers[q].mbox + kMbColl + r, seq, 0));
+    for (int q = 0; q < P; ++q) SQ_HIP(wait_seq(st, c->mbox + kMbColl + q, seq));
+    SQ_HIP(sq::p2p_fold_launch(c->coll + base, P, c->coll_cap, d, n, red, st));
+    return SQ_OK;
+}
+
+// All-reduce of n elements at d across the ranks of a one-slab-per-process
+// context (no-op for one rank and for single-process contexts).
+int rank_allreduce(sq_ctx *c, void *d, size_t n, sq::P2pRed red, hipStream_t st) {
+    if (c->p.nranks <= 1 || !per_rank(c->p.comm)) return SQ_OK;
+    if (c->p.comm == SQ_COMM_P2P) return p2p_allreduce(c, d, n, red, st);
+    if (!c->comm) return fail(SQ_E_STATE, "no RCCL communicator");
+    ncclDataType_t t = ncclFloat64;
+    ncclRedOp_t op = ncclMax;
+    switch (red) {
+    case sq::P2pRed::kMaxU32: t = ncclUint32; break;
+    case sq::P2pRed::kMaxI32: t = ncclInt32; break;
+    case sq::P2pRed::kMaxU64: t = ncclUint64; break;
+    case sq::P2pRed::kMaxF64: t = ncclFloat64; break;
+    case sq::P2pRed::kSumF64: t = ncclFloat64; op = ncclSum; break;
+    }
+    SQ_NCCL(ncclAllReduce(d, d, n, t, op, c->comm, st));
+    return SQ_OK;
+}
 
 int flush_events(sq_ctx *c) {
     for (size_t i = 0; i < c->ev_used; ++i) {
@@ -467,10 +550,16 @@ int phi4_block(sq_ctx *c, int g) {
             SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evE, 0));
         }
     }
+    const bool p2p = c->p.comm == SQ_COMM_P2P;
+    if (p2p && !c->p2p_ready) return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        if (plans[i][0].lo != 1) continue;
+        if (plans[i][0].lo != 1 && !p2p) continue;  // P2P: the neighbours always read the staged copy
         if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
+        if (p2p && c->xchg_seq > 0) {  // both neighbours have read the previous exchange's copy
+            SQ_HIP(wait_seq(s.sB, c->mbox + kMbAckFromDn, c->xchg_seq));
+            SQ_HIP(wait_seq(s.sB, c->mbox + kMbAckFromUp, c->xchg_seq));
+        }
         SQ_HIP(hipMemcpyAsync(s.stage, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
         SQ_HIP(hipMemcpyAsync(s.stage + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
         SQ_HIP(hipEventRecord(s.evS, s.sB));
@@ -491,6 +580,29 @@ int phi4_block(sq_ctx *c, int g) {
             SQ_HIP(hipEventRecord(s.evC, s.sB));
             c->perf.halo_bytes += 2.0 * (double)gbytes;
         }
+    } else if (p2p) {
+        // peer pointers: tell both neighbours our staged copy is complete, pull
+        // theirs into our ghosts (lower ghosts <- the lower neighbour's top G
+        // planes, upper ghosts <- the upper neighbour's bottom G planes), tell
+        // them we are done reading.  Flag writes run after everything before
+        // them on the stream; P = 2 (both neighbours one peer) and P = 1 (our
+        // own copy) need no special case.
+        Slab &s = c->slabs[0];
+        float *p0 = plane0(c, s, cur);
+        const int P = c->p.nranks, r = c->p.rank;
+        const int up = (r + 1) % P, dn = (r + P - 1) % P;
+        const unsigned int e = ++c->xchg_seq;
+        const size_t n = (size_t)G * plane;
+        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
+        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
+        SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromDn, e));
+        SQ_HIP(hipMemcpyAsync(p0 - n, c->peers[dn].stage + n, gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromUp, e));
+        SQ_HIP(hipMemcpyAsync(p0 + (size_t)s.nz * plane, c->peers[up].stage, gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbAckFromUp, e, 0));
+        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbAckFromDn, e, 0));
+        SQ_HIP(hipEventRecord(s.evC, s.sB));
+        c->perf.halo_bytes += 2.0 * (double)gbytes;
     } else {  // RCCL: one slab per process; this send/recv order pairs correctly for P = 2 too
         Slab &s = c->slabs[0];
         float *p0 = plane0(c, s, cur);
@@ -605,10 +717,11 @@ int phi4_autotune(sq_ctx *c, int &n) {
     }
     (void)hipEventDestroy(t0);
     (void)hipEventDestroy(t1);
-    if (c->p.comm == SQ_COMM_RCCL && c->comm != nullptr) {
+    if (per_rank(c->p.comm) && c->p.nranks > 1) {
         hipStream_t st = c->slabs[0].sA;
         SQ_HIP(hipMemcpyAsync(c->dtune, ms.data(), sizeof(double) * ms.size(), hipMemcpyHostToDevice, st));
-        SQ_NCCL(ncclAllReduce(c->dtune, c->dtune, ms.size(), ncclFloat64, ncclMax, c->comm, st));
+        int rc = rank_allreduce(c, c->dtune, ms.size(), sq::P2pRed::kMaxF64, st);
+        if (rc) return rc;
         SQ_HIP(hipMemcpyAsync(ms.data(), c->dtune, sizeof(double) * ms.size(), hipMemcpyDeviceToHost, st));
         SQ_HIP(hipStreamSynchronize(st));
     }
@@ -642,6 +755,8 @@ int phi4_steps_impl(sq_ctx *c, int n) {
         }
         return SQ_OK;
     }
+    if (c->p.comm == SQ_COMM_P2P && !c->p2p_ready)
+        return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
     if (c->g_auto && !c->g_tuned) {
         int rc = phi4_autotune(c, n);
         if (rc) return rc;
@@ -699,7 +814,7 @@ int create_phi4(sq_ctx *c) {
     {   // very large per-device fields: non-temporal output stores (mode 4) beat the
         // sc0 sc1 stores of mode 7 at 1024^3 (1575 vs 1598 us per step), not at
         // 512^3 (193.5 vs 190.8 us), profiles/r01/sweep*_sc1.log
-        const long long nz_dev = p.comm == SQ_COMM_RCCL ? (c->Lz + p.nranks - 1) / std::max(1, p.nranks) : c->Lz;
+        const long long nz_dev = per_rank(p.comm) ? (c->Lz + p.nranks - 1) / std::max(1, p.nranks) : c->Lz;
         const double field_bytes = 4.0 * c->Lx * c->Ly * (double)nz_dev;  // this device's share
         if (c->geom.pf == 7 && 2.0 * field_bytes > 2.0 * (1 << 30)) c->geom.pf = 4;
     }
@@ -716,9 +831,10 @@ int create_phi4(sq_ctx *c) {
         nslab = p.nslabs;
         if (nslab < 1 || nslab > c->Lz) return fail(SQ_E_ARG, "nslabs must be in [1, Lz]");
         for (int i = 0; i <= nslab; ++i) zs.push_back(c->Lz * i / nslab);
-    } else if (p.comm == SQ_COMM_RCCL) {
+    } else if (per_rank(p.comm)) {
         if (p.nranks < 1 || p.rank < 0 || p.rank >= p.nranks || p.nranks > c->Lz)
-            return fail(SQ_E_ARG, "bad rank/nranks for RCCL slab decomposition");
+            return fail(SQ_E_ARG, "bad rank/nranks for the slab decomposition");
+        if (p.comm == SQ_COMM_P2P && p.nranks > kP2pMaxRanks) return fail(SQ_E_ARG, "SQ_COMM_P2P: too many ranks");
         zfirst = c->Lz * p.rank / p.nranks;
         zs = {zfirst, c->Lz * (p.rank + 1) / p.nranks};
     } else {
@@ -729,7 +845,7 @@ int create_phi4(sq_ctx *c) {
     if (p.comm != SQ_COMM_NONE) {
         long long nz_min = c->Lz;
         for (int i = 0; i < nslab; ++i) nz_min = std::min(nz_min, zs[i + 1] - zs[i]);
-        if (p.comm == SQ_COMM_RCCL) nz_min = c->Lz / p.nranks;  // identical on every rank
+        if (per_rank(p.comm)) nz_min = c->Lz / p.nranks;  // identical on every rank
         // measured (profiles/r01/ghost_sweep.log, 256^3 slab, RCCL): 51.8 / 37.0 /
         // 30.4 / 26.9 / 25.6 us per step at G = 1 / 2 / 4 / 8 / 16: a fixed
         // ~28 us per exchange amortised over G steps against (G-1)/nz of
@@ -739,7 +855,7 @@ int create_phi4(sq_ctx *c) {
         // fixed cost and bandwidth of an xGMI exchange are not those of the
         // one-GPU self-exchange these defaults were measured on); SQ_GHOST
         // pins G, SQ_GHOST_AUTO=1 forces the trials on any slab path
-        c->g_auto = p.comm == SQ_COMM_RCCL && p.nranks > 1 && nz_min >= 64;
+        c->g_auto = per_rank(p.comm) && p.nranks > 1 && nz_min >= 64;
         if (const char *e = getenv("SQ_GHOST_AUTO")) c->g_auto = atoi(e) != 0;
         if (c->g_auto) g = (int)std::min(16ll, nz_min / 2);
         if (const char *e = getenv("SQ_GHOST")) {
@@ -790,6 +906,17 @@ int create_phi4(sq_ctx *c) {
         static_assert(sizeof(id.internal) <= 128, "ncclUniqueId size");
         memcpy(id.internal, p.comm_id, sizeof(id.internal));
         SQ_NCCL(ncclCommInitRank(&c->comm, p.nranks, id, p.rank));
+    }
+    if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
+        SQ_HIP(hipMalloc(&c->mbox, kMbWords * sizeof(unsigned int)));
+        SQ_HIP(hipMemset(c->mbox, 0, kMbWords * sizeof(unsigned int)));
+        const size_t need = std::max({(size_t)8 * (size_t)c->Lz, (size_t)8 * sq::kStabSlots * (size_t)std::max(1, p.loops),
+                                      (size_t)256});
+        c->coll_cap = (need + 255) / 256 * 256;
+        SQ_HIP(hipMalloc(&c->coll, 2 * (size_t)p.nranks * c->coll_cap));
+        c->peers.assign(p.nranks, Peer{});
+        c->peers[p.rank] = Peer{c->slabs[0].stage, c->mbox, c->coll, false};
+        c->p2p_ready = p.nranks == 1;  // one rank: its own buffers, nothing to map
     }
     // z chunk per wave: long enough to amortise the chunk-edge planes, short
     // enough to give >= ~8 waves per CU.
@@ -1067,8 +1194,8 @@ int phi4_field_max(sq_ctx *c, float *mx_phi, float *mx_abs) {
         SQ_HIP(hipMemsetAsync(c->dmax, 0, 2 * sizeof(unsigned int), s.sA));
         SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane_floats(c), c->dacc,
                                        c->dmax, s.sA));
-        if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1)
-            SQ_NCCL(ncclAllReduce(c->dmax, c->dmax, 2, ncclUint32, ncclMax, c->comm, s.sA));
+        int rc = rank_allreduce(c, c->dmax, 2, sq::P2pRed::kMaxU32, s.sA);
+        if (rc) return rc;
         SQ_HIP(hipMemcpyAsync(t, c->dmax, sizeof t, hipMemcpyDeviceToHost, s.sA));
         SQ_HIP(hipStreamSynchronize(s.sA));
         m[0] = std::max(m[0], t[0]);
@@ -1125,12 +1252,14 @@ int phi4_frame(sq_ctx *c, int *stable) {
     rc = phi4_join(c);
     if (rc) return rc;
     Slab &s0 = c->slabs[0];
-    if (c->p.comm == SQ_COMM_RCCL && c->p.nranks > 1) {
-        SQ_NCCL(ncclGroupStart());
-        SQ_NCCL(ncclAllReduce(c->flag, c->flag, 1, ncclInt32, ncclMax, c->comm, s0.sA));
-        SQ_NCCL(ncclAllReduce(c->st_md, c->st_md, nrec, ncclUint64, ncclMax, c->comm, s0.sA));
-        SQ_NCCL(ncclAllReduce(c->st_a, c->st_a, nrec, ncclUint32, ncclMax, c->comm, s0.sA));
-        SQ_NCCL(ncclGroupEnd());
+    if (per_rank(c->p.comm) && c->p.nranks > 1) {
+        const bool grp = c->p.comm == SQ_COMM_RCCL;
+        if (grp) SQ_NCCL(ncclGroupStart());
+        rc = rank_allreduce(c, c->flag, 1, sq::P2pRed::kMaxI32, s0.sA);
+        if (!rc) rc = rank_allreduce(c, c->st_md, nrec, sq::P2pRed::kMaxU64, s0.sA);
+        if (!rc) rc = rank_allreduce(c, c->st_a, nrec, sq::P2pRed::kMaxU32, s0.sA);
+        if (grp) SQ_NCCL(ncclGroupEnd());
+        if (rc) return rc;
     }
     int h = 0;
     std::vector<unsigned long long> md(nrec);
@@ -1236,10 +1365,34 @@ int sq_create(const sq_params *p, sq_ctx **out) {
 int sq_destroy(sq_ctx *c) {
     if (!c) return SQ_OK;
     DeviceGuard g(c->dev);
+    bool p2p_drained = true;
+    if (c->p2p_ready && c->xchg_seq > 0 && !c->slabs.empty() && c->slabs[0].sB) {
+        // P2P: our staged copy may still be read by a neighbour that is behind;
+        // free it only after both have acknowledged the last exchange (bounded
+        // wait: a peer that died leaves the buffers mapped, not a hang)
+        hipStream_t sB = c->slabs[0].sB;
+        if (wait_seq(sB, c->mbox + kMbAckFromDn, c->xchg_seq) != hipSuccess ||
+            wait_seq(sB, c->mbox + kMbAckFromUp, c->xchg_seq) != hipSuccess)
+            p2p_drained = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        while (p2p_drained && hipStreamQuery(sB) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) p2p_drained = false;
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
+    if (!p2p_drained) return SQ_OK;  // leak rather than free memory a peer may still read
     for (auto &s : c->slabs) {
         if (s.sA) (void)hipStreamSynchronize(s.sA);
         if (s.sB) (void)hipStreamSynchronize(s.sB);
     }
+    for (Peer &q : c->peers)
+        if (q.mapped) {
+            (void)hipIpcCloseMemHandle(q.stage);
+            (void)hipIpcCloseMemHandle(q.mbox);
+            (void)hipIpcCloseMemHandle(q.coll);
+        }
+    (void)hipFree(c->mbox);
+    (void)hipFree(c->coll);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &s : c->slabs) {
         (void)hipFree(s.buf[0]);
@@ -1632,6 +1785,8 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
         return SQ_OK;
     }
     if (n > c->Lz) return fail(SQ_E_ARG, "n > Lz");
+    if (c->p.comm == SQ_COMM_P2P && !c->p2p_ready)
+        return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
     int rc = phi4_join(c);
     if (rc) return rc;
     // slice sums S(z) of the whole lattice: every slab writes its planes into a
@@ -1648,10 +1803,11 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
         if (e == hipSuccess) e = sq::phi4_slices_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, d + s.z0, s.sA);
         if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
     }
-    if (e == hipSuccess && c->p.comm == SQ_COMM_RCCL && c->comm != nullptr) {
-        if (ncclAllReduce(d, d, (size_t)Lz, ncclFloat64, ncclSum, c->comm, s0) != ncclSuccess) {
+    if (e == hipSuccess && per_rank(c->p.comm) && c->p.nranks > 1) {
+        // disjoint z ranges, zeros elsewhere: the sum is exact in any order
+        if (int rc = rank_allreduce(c, d, (size_t)Lz, sq::P2pRed::kSumF64, s0)) {
             (void)hipFree(d);
-            return fail(SQ_E_COMM, "ncclAllReduce of the slice sums failed");
+            return rc;
         }
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s0);
@@ -1700,6 +1856,78 @@ int sq_comm_unique_id(unsigned char out[128]) {
     SQ_NCCL(ncclGetUniqueId(&id));
     memset(out, 0, 128);
     memcpy(out, id.internal, sizeof(id.internal));
+    return SQ_OK;
+}
+
+int sq_p2p_handle(sq_ctx *c, unsigned char out[SQ_P2P_HANDLE_BYTES]) {
+    if (!c || !out) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c) || c->p.comm != SQ_COMM_P2P) return fail(SQ_E_STATE, "not an SQ_COMM_P2P context");
+    DeviceGuard g(c->dev);
+    P2pBlob b{};
+    b.magic = kP2pMagic;
+    b.version = SQ_ABI_VERSION;
+    b.rank = c->p.rank;
+    b.nranks = c->p.nranks;
+    b.Lx = c->Lx;
+    b.Ly = c->Ly;
+    b.gpad = c->gpad;
+    b.Lz = c->Lz;
+    b.coll_cap = (long long)c->coll_cap;
+    b.seed = c->p.seed;
+    SQ_HIP(hipIpcGetMemHandle(&b.stage, c->slabs[0].stage));
+    SQ_HIP(hipIpcGetMemHandle(&b.mbox, c->mbox));
+    SQ_HIP(hipIpcGetMemHandle(&b.coll, c->coll));
+    memset(out, 0, SQ_P2P_HANDLE_BYTES);
+    memcpy(out, &b, sizeof b);
+    return SQ_OK;
+}
+
+int sq_p2p_connect(sq_ctx *c, const unsigned char *handles, int nranks) {
+    if (!c || !handles) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c) || c->p.comm != SQ_COMM_P2P) return fail(SQ_E_STATE, "not an SQ_COMM_P2P context");
+    if (nranks != c->p.nranks) return fail(SQ_E_ARG, "handle count != nranks");
+    if (c->p2p_ready && nranks > 1) return fail(SQ_E_STATE, "already connected");
+    if (nranks == 1) return SQ_OK;
+    std::vector<P2pBlob> bl(nranks);
+    for (int q = 0; q < nranks; ++q) {  // validate every blob before mapping anything
+        memcpy(&bl[q], handles + (size_t)q * SQ_P2P_HANDLE_BYTES, sizeof(P2pBlob));
+        const P2pBlob &b = bl[q];
+        if (b.magic != kP2pMagic || b.version != SQ_ABI_VERSION) return fail(SQ_E_ARG, "not a P2P handle blob");
+        if (b.rank != q || b.nranks != nranks)
+            return fail(SQ_E_ARG, "handle " + std::to_string(q) + " belongs to rank " + std::to_string(b.rank) +
+                                      " of " + std::to_string(b.nranks) + " (blobs must be in rank order)");
+        if (b.Lx != c->Lx || b.Ly != c->Ly || b.Lz != c->Lz || b.gpad != c->gpad ||
+            b.coll_cap != (long long)c->coll_cap || b.seed != c->p.seed)
+            return fail(SQ_E_ARG, "rank " + std::to_string(q) + " was created for a different lattice, ghost depth or seed");
+    }
+    DeviceGuard g(c->dev);
+    for (int q = 0; q < nranks; ++q) {
+        if (q == c->p.rank) continue;
+        Peer pr{};
+        void *a = nullptr, *m = nullptr, *k = nullptr;
+        hipError_t e = hipIpcOpenMemHandle(&a, bl[q].stage, hipIpcMemLazyEnablePeerAccess);
+        if (e == hipSuccess) e = hipIpcOpenMemHandle(&m, bl[q].mbox, hipIpcMemLazyEnablePeerAccess);
+        if (e == hipSuccess) e = hipIpcOpenMemHandle(&k, bl[q].coll, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+            for (void *v : {a, m, k})
+                if (v) (void)hipIpcCloseMemHandle(v);
+            for (Peer &o : c->peers)
+                if (o.mapped) {
+                    (void)hipIpcCloseMemHandle(o.stage);
+                    (void)hipIpcCloseMemHandle(o.mbox);
+                    (void)hipIpcCloseMemHandle(o.coll);
+                    o = Peer{};
+                }
+            return fail(SQ_E_COMM, std::string("hipIpcOpenMemHandle (rank ") + std::to_string(q) + "): " +
+                                       hipGetErrorString(e));
+        }
+        pr.stage = static_cast<float *>(a);
+        pr.mbox = static_cast<unsigned int *>(m);
+        pr.coll = static_cast<unsigned char *>(k);
+        pr.mapped = true;
+        c->peers[q] = pr;
+    }
+    c->p2p_ready = true;
     return SQ_OK;
 }
 

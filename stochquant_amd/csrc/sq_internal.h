@@ -84,6 +84,12 @@ hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsi
 hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double *out,
                               hipStream_t s);
 
+// Peer-pointer transport (sq_p2p.hip): out[i] = fold over q < nranks of
+// slot q's element i, slot q at slots + q * cap bytes, in rank order.
+enum class P2pRed { kMaxU32, kMaxI32, kMaxU64, kMaxF64, kSumF64 };
+hipError_t p2p_fold_launch(const unsigned char *slots, int nranks, size_t cap, void *out, size_t n, P2pRed red,
+                           hipStream_t s);
+
 // ---------------------------------------------------------------- QM1D ----
 struct Qm1dState {    // device-resident frame scalars
     double omega_in;  // ω at frame start

@@ -19,7 +19,7 @@ import subprocess
 import numpy as np
 
 from . import _lib
-from ._lib import (SQ_COMM_LOOPBACK, SQ_COMM_NONE, SQ_COMM_RCCL, SQ_MODEL_PHI4, SQ_MODEL_QM1D, SQ_ORDER_JACOBI,
+from ._lib import (SQ_COMM_LOOPBACK, SQ_COMM_NONE, SQ_COMM_P2P, SQ_COMM_RCCL, SQ_MODEL_PHI4, SQ_MODEL_QM1D, SQ_ORDER_JACOBI,
                    SQ_ORDER_SERIAL)
 
 _DP = ctypes.POINTER(ctypes.c_double)
@@ -188,6 +188,11 @@ class Phi4Lattice(_Ctx):
     comm="loopback" `nslabs` slabs on one device, halos by D2D copies
     comm="rccl"     one slab per process (rank / nranks), halos over RCCL;
                     `comm_id` from `unique_id()` on rank 0
+    comm="p2p"      one slab per process, halos pulled from the neighbours'
+                    memory (IPC peer pointers), no RCCL; every rank passes
+                    all ranks' `p2p_handle()` blobs, in rank order, to
+                    `p2p_connect` before stepping (`connect_p2p` does it over
+                    a torch.distributed group)
     """
 
     def __init__(self, shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, device=0, comm="none",
@@ -206,7 +211,7 @@ class Phi4Lattice(_Ctx):
         p.loops = int(loops)
         p.C = float(C)
         p.adapt_dtau = 1 if adapt_dtau else 0
-        p.comm = {"none": SQ_COMM_NONE, "loopback": SQ_COMM_LOOPBACK, "rccl": SQ_COMM_RCCL}[comm]
+        p.comm = {"none": SQ_COMM_NONE, "loopback": SQ_COMM_LOOPBACK, "rccl": SQ_COMM_RCCL, "p2p": SQ_COMM_P2P}[comm]
         p.nslabs = int(nslabs)
         p.nranks = int(nranks)
         p.rank = int(rank)
@@ -292,6 +297,28 @@ class Phi4Lattice(_Ctx):
         out = np.empty(n)
         _lib.call("sq_correlator", self._h, _dptr(out), n)
         return out
+
+    def p2p_handle(self):
+        """This rank's SQ_COMM_P2P handle blob (bytes) for the other ranks."""
+        buf = (ctypes.c_ubyte * _lib.SQ_P2P_HANDLE_BYTES)()
+        _lib.call("sq_p2p_handle", self._h, buf)
+        return bytes(buf)
+
+    def p2p_connect(self, blobs):
+        """Map the peers of an SQ_COMM_P2P context: `blobs` = every rank's p2p_handle(), in rank order."""
+        n = _lib.SQ_P2P_HANDLE_BYTES
+        if any(len(b) != n for b in blobs):
+            raise ValueError(f"every handle blob has {n} bytes")
+        buf = (ctypes.c_ubyte * (n * len(blobs))).from_buffer_copy(b"".join(blobs))
+        _lib.call("sq_p2p_connect", self._h, buf, len(blobs))
+
+
+def connect_p2p(lat, group=None):
+    """All-gather the ranks' P2P handle blobs over torch.distributed and connect."""
+    import torch.distributed as dist
+    blobs = [None] * dist.get_world_size(group)
+    dist.all_gather_object(blobs, lat.p2p_handle(), group=group)
+    lat.p2p_connect(blobs)
 
 
 def unique_id():

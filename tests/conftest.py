@@ -13,6 +13,25 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libstochquant.so)")
+    # The multi-process P2P tests fork their rank processes from a fork server
+    # started here, before this process makes its first HIP call: a process
+    # that has initialised the GPU must never fork+exec (tests/p2p_ranks.py).
+    global _FORKSERVER
+    if "not gpu" not in config.getoption("markexpr", ""):
+        import multiprocessing.forkserver
+        multiprocessing.forkserver.ensure_running()
+        _FORKSERVER = True
+
+
+_FORKSERVER = False
+
+
+def rank_context():
+    """multiprocessing context of the P2P rank processes (see pytest_configure)."""
+    import multiprocessing
+    if not _FORKSERVER:
+        pytest.fail("the rank fork server was not started before the first HIP call")
+    return multiprocessing.get_context("forkserver")
 
 
 def golden(name):

@@ -1,0 +1,52 @@
+"""Rank processes of the multi-process SQ_COMM_P2P tests (tests/test_gpu_p2p.py).
+
+The ranks are forked by a multiprocessing fork server that conftest.py starts
+before the test process touches the GPU, so no process that has initialised
+HIP ever forks+execs.  Each rank creates its slab context, sends its handle
+blob to the parent, receives every rank's blob, connects, runs the script the
+test gave it and sends back what it observed.
+"""
+import os
+import traceback
+
+
+def rank_main(conn, rank, nranks, shape, kw, env, script):
+    lat = None
+    try:
+        os.environ.update(env)
+        from stochquant_amd import Phi4Lattice
+        lat = Phi4Lattice(shape, comm="p2p", nranks=nranks, rank=rank, device=0, **kw)
+        conn.send(("blob", lat.p2p_handle()))
+        blobs = conn.recv()
+        lat.p2p_connect(blobs)
+        out = {"z0": lat.z0, "nz": lat.nz_local, "ghost": lat.ghost}
+        for op, arg in script:
+            if op == "upload":
+                lat.upload(arg[lat.z0:lat.z0 + lat.nz_local])
+            elif op == "step":
+                lat.step(arg)
+            elif op == "frame":
+                out.setdefault("stable", []).append(bool(lat.run_frame()))
+                out.setdefault("dtau", []).append(lat.dtau)
+                st = lat.stability()
+                out.setdefault("fired", []).append(st["fired"])
+                out.setdefault("TV", []).append((float(st["T"]), float(st["V"])))
+            elif op == "field":
+                out.setdefault("field", []).append(lat.download())
+            elif op == "correlator":
+                out["correlator"] = lat.correlator(arg)
+            elif op == "ghost":
+                out["ghost"] = lat.ghost
+            else:
+                raise ValueError(op)
+        out["step_counter"] = lat.step_counter
+        out["perf"] = lat.perf()
+        lat.close()
+        lat = None
+        conn.send(("ok", out))
+    except Exception:  # reported to the parent, which fails the test
+        conn.send(("error", traceback.format_exc()))
+    finally:
+        if lat is not None:
+            lat.close()
+        conn.close()
