@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SQ_ABI_VERSION 2
+#define SQ_ABI_VERSION 3
 
 /* status codes */
 #define SQ_OK 0
@@ -85,20 +85,25 @@ typedef struct sq_perf_t {
 } sq_perf_t;
 
 /* One operation of a deep-halo block (PHI4 slab decompositions),
- * in issue order; see sq_phi4_block_plan. */
-#define SQ_OP_EXCHANGE 0       /* stream B: after the previous block's SQ_OP_EDGES_DONE, send the ghost-depth
-                                  edge planes of the latest field to both z-neighbours, receive their ghosts */
-#define SQ_OP_STEP 1           /* stream A: step `step` on planes [lo, hi) (and [lo2, hi2) when lo2 < hi2) */
-#define SQ_OP_PAIR 2           /* stream A: steps `step`, `step`+1 in one launch; output [lo, hi), reads
-                                  [lo-2, hi+2) of the latest field */
-#define SQ_OP_WAIT_EXCHANGE 3  /* stream A waits for this block's exchange */
-#define SQ_OP_EDGES_DONE 4     /* stream A: the planes the next exchange sends are final (event) */
-#define SQ_OP_WAIT_STAGED 5    /* stream A waits until the exchange has copied its edge planes aside (an
-                                  EXCHANGE op with lo = 1 sends from that staged copy) */
+ * in an issue order that is also a valid sequential order; each op runs on
+ * stream A (interior, stream = 0) or stream B (exchange and rims, stream = 1).
+ * See sq_phi4_block_plan. */
+#define SQ_OP_EXCHANGE 0       /* after the previous block's SQ_OP_EDGES_DONE, send the ghost-depth edge
+                                  planes of the latest field to both z-neighbours, receive their ghosts */
+#define SQ_OP_STEP 1           /* step `step` on planes [lo, hi) (and [lo2, hi2) when lo2 < hi2) */
+#define SQ_OP_PAIR 2           /* steps `step`, `step`+1 in one launch; output [lo, hi), reads [lo-2, hi+2)
+                                  of the field the previous launch group wrote */
+#define SQ_OP_WAIT_EXCHANGE 3  /* waits for this block's exchange (and, loopback, the neighbours') */
+#define SQ_OP_EDGES_DONE 4     /* the planes the next exchange sends are final (event) */
+#define SQ_OP_WAIT_STAGED 5    /* waits until the exchange has copied its edge planes aside (an EXCHANGE
+                                  op with lo = 1 sends from that staged copy) */
+#define SQ_OP_SIGNAL 6         /* records event slot `lo` on the op's stream */
+#define SQ_OP_WAIT 7           /* the op's stream waits for event slot `lo` */
 typedef struct sq_block_op {
     int kind;                  /* SQ_OP_* */
     int step;                  /* block-relative index of the (first) step computed */
     int lo, hi, lo2, hi2;      /* local plane ranges; negative = lower ghost zone, >= nz = upper */
+    int stream;                /* 0: stream A (interior), 1: stream B (exchange, rims) */
 } sq_block_op;
 
 typedef struct sq_ctx sq_ctx;
@@ -173,13 +178,14 @@ int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
  * needed; the product's phi4_block executes exactly this list): a slab of nz
  * planes with a ghost zone of `ghost` planes (the exchange depth G) running
  * g <= G steps; fuse2 != 0 runs the steps as two-step pairs, the first
- * core_pairs of them on the ghost-free core ahead of the exchange; edge_first
- * != 0 computes the last step's edge planes first.  Writes *nops ops (at most
- * cap).  sq_phi4_pick_ghost returns the index of the fastest candidate of the
+ * core_pairs of them on the ghost-free core ahead of the exchange (0: no
+ * core/rim split, the first launch waits for the exchange), their rims on the
+ * exchange stream when rims_b != 0; edge_first != 0 computes the last step's
+ * edge planes first.  Writes *nops ops (at most cap).  sq_phi4_pick_ghost returns the index of the fastest candidate of the
  * rank-max-reduced per-step times ms[n] (the ghost-depth trial, identical on
  * every rank once the times are reduced). */
-int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, sq_block_op *ops,
-                       int cap, int *nops);
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, int rims_b,
+                       sq_block_op *ops, int cap, int *nops);
 int sq_phi4_pick_ghost(const double *ms, int n);
 /* PHI4 frame stability (the heuristic of tau_kernel.cl:135-143 restated for
  * the 3-D lattice).  Every frame records per step j the maximum

@@ -74,11 +74,12 @@ class SqPerf(ctypes.Structure):
 
 class SqBlockOp(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("step", ctypes.c_int), ("lo", ctypes.c_int), ("hi", ctypes.c_int),
-                ("lo2", ctypes.c_int), ("hi2", ctypes.c_int)]
+                ("lo2", ctypes.c_int), ("hi2", ctypes.c_int), ("stream", ctypes.c_int)]
 
 
-SQ_OP_EXCHANGE, SQ_OP_STEP, SQ_OP_PAIR, SQ_OP_WAIT_EXCHANGE, SQ_OP_EDGES_DONE, SQ_OP_WAIT_STAGED = range(6)
-ABI_VERSION = 2
+(SQ_OP_EXCHANGE, SQ_OP_STEP, SQ_OP_PAIR, SQ_OP_WAIT_EXCHANGE, SQ_OP_EDGES_DONE, SQ_OP_WAIT_STAGED, SQ_OP_SIGNAL,
+ SQ_OP_WAIT) = range(8)
+ABI_VERSION = 3
 
 
 _P = ctypes.c_void_p
@@ -111,7 +112,7 @@ SIGNATURES = {
     "sq_phi4_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "sq_phi4_ghost": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "sq_phi4_block_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_int, ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
+                                          ctypes.c_int, ctypes.c_int, ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
     "sq_phi4_pick_ghost": (ctypes.c_int, [_D, ctypes.c_int]),
     "sq_phi4_stability": (ctypes.c_int, [_P, _D, _I, _F, _F, _F, ctypes.c_int]),
     "sq_phi4_set_stability": (ctypes.c_int, [_P, ctypes.c_double, ctypes.c_double]),

@@ -66,10 +66,11 @@ struct Slab {
     int nz = 0;
     long long z0 = 0;
     hipStream_t sA = nullptr, sB = nullptr;
-    hipEvent_t evA = nullptr, evC = nullptr;  // A: block's steps done; C: its halo exchange done
+    hipEvent_t evC = nullptr;                 // C: the block's halo exchange done
     hipEvent_t evE = nullptr;                 // E: the block's output edge planes (what the next exchange sends) done
     float *stage = nullptr;                   // 2 G planes: the staged copy of the edge planes an exchange sends
     hipEvent_t evS = nullptr;                 // S: the staged copy is complete (the field's edges may change)
+    std::vector<hipEvent_t> evk;              // the block plan's SIGNAL / WAIT slots (kPlanSlots)
 };
 
 struct EvPair {
@@ -172,7 +173,8 @@ struct sq_ctx {
     bool field_finite = true;  // every plane of the current field has been through the guard (or
                                // came from sq_init_field); false after a caller's upload / load
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
-    int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange
+    int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
+    bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
                             // (SQ_CORE_PAIRS pins; multi-rank runs time 1, 2, 4 on the real link)
     double *dacc = nullptr;
     unsigned int *dmax = nullptr;  // [0] max |phi| bits, [1] ordered max phi
@@ -437,71 +439,97 @@ int phi4_periodic_step(sq_ctx *c) {
 }
 
 // The schedule of a deep-halo block of g <= G steps on a slab of nz planes
-// with a ghost zone of G planes:
+// with a ghost zone of G planes.  Each op names its stream:
+// A (interior) or B (exchange, and the rims when rims_b).
 //   EXCHANGE     stream B, after the previous block's EDGES_DONE: G edge planes
-//                of the block's input field to both z-neighbours, their ghosts in;
-//   then stream A.  Step k updates the shrinking extended range
-//   [-(g-1-k), nz+g-1-k), recomputing ghost-zone sites.  With fuse2 (two steps
-//   per launch) and g >= 3 every step runs in pairs, and the first K pairs
-//   (kc = core pairs) are split around the exchange:
-//     PAIR 2j core  step 2j+1 on [2j+2, nz-2j-2), j < K: reads no ghost (step s
-//                   is valid without ghosts on [s+1, nz-s-1)), so all K of them
-//                   overlap the exchange;
-//     WAIT_EXCHANGE;
-//     PAIR 2j rim   step 2j+1 on [-(g-2-2j), 2j+2) u [nz-2j-2, nz+g-2-2j), j < K
-//                   (two ranges of g planes, one launch);
-//     PAIR s        the remaining pairs on step s+1's whole range, reading step s-1's;
+//                of the block's input field to both z-neighbours, their ghosts in.
+//   Step k updates the shrinking extended range [-(g-1-k), nz+g-1-k),
+//   recomputing ghost-zone sites.  With fuse2 (two steps per launch) and g >= 3
+//   every step runs in pairs, and the first K pairs (kc = core pairs) are split:
+//     PAIR 2j core  stream A, step 2j+1 on [2j+2, nz-2j-2), j < K: reads no ghost
+//                   (step s is valid without ghosts on [s+1, nz-s-1)), so the
+//                   core pairs overlap the exchange;
+//     PAIR 2j rim   step 2j+1 on [-(g-2-2j), 2j+2) u [nz-2j-2, nz+g-2-2j) (two
+//                   ranges, one launch), either on stream A after WAIT_EXCHANGE
+//                   (short exchanges: no cross-stream hop before the next pair),
+//                   or, rims_b, on stream B right behind the exchange, rim j > 0
+//                   after core j-1 (SIGNAL A / WAIT B on slot j-1), stream A
+//                   continuing once they are in (SIGNAL B / WAIT A on kRimSlot):
+//                   long exchanges then overlap the cores with the rims too;
+//     K = 0: no split -- stream A waits for the exchange and the first pair
+//                   covers the whole range (an exchange shorter than the
+//                   previous block's last middle pair is then hidden for free);
+//     PAIR s        stream A, the remaining pairs on step s+1's whole range;
 //     the last pair (or single step) computes its edge planes [0, G) u
 //     [nz-G, nz) first and marks EDGES_DONE, so the NEXT block's exchange
 //     overlaps this step's middle as well as the next cores (when the core
-//     pairs reach the last step, its middle is done before the exchange and
-//     EDGES_DONE follows the last rims);
-//   without fuse2 (or g < 3) step 0 is a single-step core [1, nz-1) / rim
-//   [-(g-1), 1) u [nz-1, nz+g-1) split and the later steps single launches.
+//     pairs reach the last step, EDGES_DONE follows the rims);
+//   without fuse2 (or g < 3) step 0 is a single-step core [1, nz-1) and rim
+//   [-(g-1), 1) u [nz-1, nz+g-1) (K = 0: one span), the later steps single
+//   launches on A.
 // Ghost-zone sites are recomputed redundantly; the counter-based noise makes
 // them bit-identical to their owner's, so the result equals the monolithic run.
-// Buffers: pair j writes step 2j+1 into the other buffer of step 2j-1's; a
-// core pair running ahead of the rims only writes [2j+2, nz-2j-2), which no
-// earlier rim pair reads ([.., 2i+4) u [nz-2i-4, ..) for i < j).
-std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first, int kc) {
+// Buffers: a launch group (the ops of one first step) reads the buffer of the
+// step before it and writes the other (phi4_block counts the groups); a core
+// pair running ahead of the rims only writes [2j+2, nz-2j-2), which no earlier
+// rim pair reads ([.., 2i+4) u [nz-2i-4, ..) for i < j).
+constexpr int kPlanSlots = 16;            // events per slab the plan's SIGNAL / WAIT ops name
+constexpr int kRimSlot = kPlanSlots - 1;  // the rims of the block are done
+constexpr int kA = 0, kB = 1;
+
+std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_first, int kc, bool rims_b) {
     std::vector<sq_block_op> ops;
-    auto add = [&](int kind, int step, int lo, int hi, int lo2 = 0, int hi2 = 0) {
-        ops.push_back(sq_block_op{kind, step, lo, hi, lo2, hi2});
+    auto add = [&](int kind, int step, int lo, int hi, int lo2, int hi2, int stream) {
+        ops.push_back(sq_block_op{kind, step, lo, hi, lo2, hi2, stream});
+    };
+    const int rs = rims_b ? kB : kA;  // the rims' stream
+    auto rims_done = [&]() {
+        if (!rims_b) return;
+        add(SQ_OP_SIGNAL, 0, kRimSlot, 0, 0, 0, kB);
+        add(SQ_OP_WAIT, 0, kRimSlot, 0, 0, 0, kA);
     };
     const bool split_edges = edge_first && nz > 2 * G;
-    add(SQ_OP_EXCHANGE, 0, 0, 0);
+    add(SQ_OP_EXCHANGE, 0, 0, 0, 0, 0, kB);
     int st;
     bool edges = false;
-    if (fuse2 && g >= 3) {
+    if (kc <= 0) {  // no core/rim split
+        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0, 0, 0, kA);
+        st = 0;
+    } else if (fuse2 && g >= 3) {
         // core pairs: at least one, at most the pairs of the block, and only
         // while the core is not empty
-        int K = std::max(1, std::min(kc, g / 2));
+        int K = std::max(1, std::min(std::min(kc, g / 2), kRimSlot));
         while (K > 1 && nz <= 4 * K) --K;
         // core pair 1 writes step 3 into the buffer the exchange sends its edge
         // planes from: with K >= 2 the exchange sends a staged copy of them, and
         // core pair 1 waits only for that copy
         if (K >= 2) ops[0].lo = 1;
-        for (int j = 0; j < K && nz > 4 * j + 4; ++j) {
-            if (j == 1) add(SQ_OP_WAIT_STAGED, 0, 0, 0);
-            add(SQ_OP_PAIR, 2 * j, 2 * j + 2, nz - 2 * j - 2);
+        int nc = 0;
+        for (int j = 0; j < K && nz > 4 * j + 4; ++j, ++nc) {
+            if (j == 1) add(SQ_OP_WAIT_STAGED, 0, 0, 0, 0, 0, kA);
+            add(SQ_OP_PAIR, 2 * j, 2 * j + 2, nz - 2 * j - 2, 0, 0, kA);
+            if (rims_b && j + 1 < K) add(SQ_OP_SIGNAL, 2 * j, j, 0, 0, 0, kA);
         }
-        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
+        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0, 0, 0, rs);
         for (int j = 0; j < K; ++j) {
+            if (rims_b && j > 0 && j - 1 < nc) add(SQ_OP_WAIT, 2 * j, j - 1, 0, 0, 0, kB);
             const int lo_a = -(g - 2 - 2 * j), hi_a = 2 * j + 2, lo_b = nz - 2 * j - 2, hi_b = nz + g - 2 - 2 * j;
             if (hi_a >= lo_b)  // rims meet (no core): one span
-                add(SQ_OP_PAIR, 2 * j, lo_a, hi_b);
+                add(SQ_OP_PAIR, 2 * j, lo_a, hi_b, 0, 0, rs);
             else
-                add(SQ_OP_PAIR, 2 * j, lo_a, hi_a, lo_b, hi_b);
+                add(SQ_OP_PAIR, 2 * j, lo_a, hi_a, lo_b, hi_b, rs);
         }
+        rims_done();
         st = 2 * K;
     } else {
-        if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1);
-        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0);
+        if (nz - 1 > 1) add(SQ_OP_STEP, 0, 1, nz - 1, 0, 0, kA);
+        add(SQ_OP_WAIT_EXCHANGE, 0, 0, 0, 0, 0, rs);
         const int lo_a = -(g - 1), hi_a = 1, lo_b = nz - 1, hi_b = nz + g - 1;
         if (hi_a >= lo_b)  // rims meet (nz <= 2): one span
-            add(SQ_OP_STEP, 0, lo_a, hi_b);
+            add(SQ_OP_STEP, 0, lo_a, hi_b, 0, 0, rs);
         else
-            add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b);
+            add(SQ_OP_STEP, 0, lo_a, hi_a, lo_b, hi_b, rs);
+        rims_done();
         st = 1;
     }
     while (st < g) {
@@ -509,17 +537,17 @@ std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_
         const int last = pair ? st + 1 : st;  // the step this op group completes
         const int kind = pair ? SQ_OP_PAIR : SQ_OP_STEP;
         if (last == g - 1 && split_edges) {
-            add(kind, st, 0, G, nz - G, nz);
-            add(SQ_OP_EDGES_DONE, st, 0, 0);
-            add(kind, st, G, nz - G);
+            add(kind, st, 0, G, nz - G, nz, kA);
+            add(SQ_OP_EDGES_DONE, st, 0, 0, 0, 0, kA);
+            add(kind, st, G, nz - G, 0, 0, kA);
             edges = true;
         } else {
             const int e = g - 1 - last;  // ghost planes the completed step still updates on either side
-            add(kind, st, -e, nz + e);
+            add(kind, st, -e, nz + e, 0, 0, kA);
         }
         st = last + 1;
     }
-    if (!edges) add(SQ_OP_EDGES_DONE, g - 1, 0, 0);
+    if (!edges) add(SQ_OP_EDGES_DONE, g - 1, 0, 0, 0, 0, kA);
     return ops;
 }
 
@@ -531,7 +559,7 @@ int phi4_block(sq_ctx *c, int g) {
     const int cur = c->cur;
     const unsigned long long step0 = c->step;
     std::vector<std::vector<sq_block_op>> plans;
-    for (const Slab &s : c->slabs) plans.push_back(block_plan(s.nz, G, g, c->tbz > 0, c->edge_first, c->core_pairs));
+    for (const Slab &s : c->slabs) plans.push_back(block_plan(s.nz, G, g, c->tbz > 0, c->edge_first, c->core_pairs, c->rims_b));
     // 1. exchange (stream B), for every slab before any slab waits for one;
     //    staged (EXCHANGE op lo = 1): the edge planes are copied aside first and
     //    sent from the copy, so the block's core pairs may overwrite them early
@@ -618,50 +646,57 @@ int phi4_block(sq_ctx *c, int g) {
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     }
-    // 2. the rest of the schedule, slab by slab (each slab has its own stream A;
+    // 2. the rest of the schedule, slab by slab (each slab has its own streams;
     //    slabs of a loopback decomposition may differ in nz, hence in schedule)
     int out_buf = cur;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
         const std::vector<sq_block_op> &ops = plans[i];
-        int in = cur;            // buffer holding the latest completed step
-        bool flip = false;       // the current op group writes in ^ 1
-        int gstep = -1, gkind = -1;  // the current op group: ops of one kind and step read the same buffer
+        // launch groups: the ops of one first step read the buffer written by
+        // the group before (every group flips the parity once)
+        std::vector<int> starts;
+        for (const sq_block_op &op : ops)
+            if (op.kind == SQ_OP_STEP || op.kind == SQ_OP_PAIR) starts.push_back(op.step);
+        std::sort(starts.begin(), starts.end());
+        starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
+        std::vector<char> timed(starts.size(), 0);
         for (const sq_block_op &op : ops) {
             int rc = SQ_OK;
+            hipStream_t st = op.stream == kB ? s.sB : s.sA;
             if (op.kind == SQ_OP_STEP || op.kind == SQ_OP_PAIR) {
-                const bool first = op.step != gstep || op.kind != gkind;  // it carries the group's timing
-                if (first) {
-                    if (flip) in ^= 1;
-                    flip = true;
-                    gstep = op.step;
-                    gkind = op.kind;
-                }
+                const size_t gi = (size_t)(std::lower_bound(starts.begin(), starts.end(), op.step) - starts.begin());
+                const int in = cur ^ (int)(gi & 1);
+                const bool first = !timed[gi];  // it carries the group's timing
+                timed[gi] = 1;
                 c->step = step0 + (unsigned long long)op.step;
                 if (op.kind == SQ_OP_PAIR)
-                    rc = phi4_tb2_range(c, s, in, s.sA, op.lo, op.hi, op.lo2, op.hi2, 0, first);
+                    rc = phi4_tb2_range(c, s, in, st, op.lo, op.hi, op.lo2, op.hi2, 0, first);
                 else if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
-                    rc = phi4_launch_range(c, s, in, s.sA, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
+                    rc = phi4_launch_range(c, s, in, st, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
                 else
-                    rc = phi4_launch_span(c, s, in, s.sA, op.lo, op.hi, first);
+                    rc = phi4_launch_span(c, s, in, st, op.lo, op.hi, first);
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
-                SQ_HIP(hipStreamWaitEvent(s.sA, s.evC, 0));
+                if (op.stream != kB) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));  // B: ordered behind its exchange
                 if (c->p.comm == SQ_COMM_LOOPBACK) {
-                    SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + ns - 1) % ns].evC, 0));
-                    SQ_HIP(hipStreamWaitEvent(s.sA, c->slabs[(i + 1) % ns].evC, 0));
+                    SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + ns - 1) % ns].evC, 0));
+                    SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + 1) % ns].evC, 0));
                 }
             } else if (op.kind == SQ_OP_WAIT_STAGED) {
-                SQ_HIP(hipStreamWaitEvent(s.sA, s.evS, 0));
+                SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));
             } else if (op.kind == SQ_OP_EDGES_DONE) {
-                SQ_HIP(hipEventRecord(s.evE, s.sA));
+                SQ_HIP(hipEventRecord(s.evE, st));
+            } else if (op.kind == SQ_OP_SIGNAL || op.kind == SQ_OP_WAIT) {
+                if (op.lo < 0 || op.lo >= kPlanSlots) return fail(SQ_E_STATE, "block op event slot out of range");
+                if (op.kind == SQ_OP_SIGNAL)
+                    SQ_HIP(hipEventRecord(s.evk[op.lo], st));
+                else
+                    SQ_HIP(hipStreamWaitEvent(st, s.evk[op.lo], 0));
             } else if (op.kind != SQ_OP_EXCHANGE) {  // the exchange was issued above for every slab
                 return fail(SQ_E_STATE, "unknown block op");
             }
             if (rc) return rc;
         }
-        if (flip) in ^= 1;
-        SQ_HIP(hipEventRecord(s.evA, s.sA));
-        out_buf = in;
+        out_buf = cur ^ (int)(starts.size() & 1);
     }
     c->step = step0;
     for (int k = 0; k < g; ++k) count_step(c);
@@ -673,22 +708,29 @@ int phi4_join(sq_ctx *c);
 
 // Ghost depth by measurement (slab paths): G in {4, 8, 16} (<= the allocated
 // depth), each timed over two blocks after one warm-up block on the interior
-// stream; across ranks the per-candidate times are max-reduced over RCCL so
-// every rank picks the same G (exchange sizes must match).  The trial steps
-// are ordinary steps: the field is the same for any G.
+// stream; across ranks the per-candidate times are max-reduced (RCCL or peer
+// memory) so every rank picks the same G (exchange sizes must match).  With
+// fused pairs the deepest zone is also tried without a core/rim split (K = 0)
+// and with K = 2, 4 core pairs, rims on A or on the exchange stream.  The
+// trial steps are ordinary steps: the field is the same for any schedule
+// (DESIGN.md §8).
 int phi4_autotune(sq_ctx *c, int &n) {
     struct Cand {
         int g, k;
+        bool rb;
     };
     std::vector<Cand> cand;
     for (int g : {4, 8, 16})
-        if (g <= c->gpad) cand.push_back({g, c->core_pairs});
-    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs});
-    // with fused pairs, how many core pairs run ahead of the exchange: the
-    // deepest ghost zone's block tried with 2 and 4 as well
-    if (c->tbz > 0 && c->k_auto)
-        for (int k : {2, 4})
-            if (k <= cand.back().g / 2) cand.push_back({cand.back().g, k});
+        if (g <= c->gpad) cand.push_back({g, c->core_pairs, c->rims_b});
+    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs, c->rims_b});
+    if (c->tbz > 0 && c->k_auto) {
+        const int gd = cand.back().g;
+        cand.push_back({gd, 0, false});
+        for (bool rb : {false, true})
+            for (int k : {2, 4})
+                if (k <= gd / 2) cand.push_back({gd, k, rb});
+    }
+    if (cand.size() > 16) cand.resize(16);  // dtune holds 16 times
     int need = 0;
     for (const Cand &k : cand) need += 3 * k.g;
     if (n < need) return SQ_OK;  // too few steps requested: try again on a later call
@@ -700,6 +742,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
         const int g = cand[k].g;
         c->gz = g;
         c->core_pairs = cand[k].k;
+        c->rims_b = cand[k].rb;
         int rc = phi4_block(c, g);
         if (!rc) rc = phi4_join(c);
         if (rc) return rc;
@@ -728,6 +771,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
     const Cand best = cand[(size_t)sq_phi4_pick_ghost(ms.data(), (int)ms.size())];
     c->gz = best.g;
     c->core_pairs = best.k;
+    c->rims_b = best.rb;
     c->g_tuned = true;
     return SQ_OK;
 }
@@ -871,7 +915,7 @@ int create_phi4(sq_ctx *c) {
         }
         c->gz = (int)std::max(1ll, std::min((long long)g, nz_min));
         c->gpad = c->gz;
-        SQ_HIP(hipMalloc(&c->dtune, 8 * sizeof(double)));
+        SQ_HIP(hipMalloc(&c->dtune, 16 * sizeof(double)));
     }
     const size_t plane = plane_floats(c);
     for (int i = 0; i < nslab; ++i) {
@@ -891,12 +935,12 @@ int create_phi4(sq_ctx *c) {
         int prio_lo = 0, prio_hi = 0;
         SQ_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
         SQ_HIP(hipStreamCreateWithPriority(&s.sB, hipStreamNonBlocking, prio_hi));
-        SQ_HIP(hipEventCreateWithFlags(&s.evA, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evC, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evE, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evS, hipEventDisableTiming));
+        s.evk.assign(kPlanSlots, nullptr);
+        for (hipEvent_t &e : s.evk) SQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         if (p.comm != SQ_COMM_NONE) SQ_HIP(hipMalloc(&s.stage, 2 * (size_t)c->gpad * plane * sizeof(float)));
-        SQ_HIP(hipEventRecord(s.evA, s.sA));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         SQ_HIP(hipEventRecord(s.evE, s.sA));
     }
@@ -940,7 +984,11 @@ int create_phi4(sq_ctx *c) {
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
     if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
     if (const char *e = getenv("SQ_CORE_PAIRS")) {
-        c->core_pairs = std::max(1, atoi(e));
+        c->core_pairs = std::max(0, atoi(e));
+        c->k_auto = false;
+    }
+    if (const char *e = getenv("SQ_RIMS_B")) {
+        c->rims_b = atoi(e) != 0;
         c->k_auto = false;
     }
     c->zc = zc;
@@ -1407,10 +1455,11 @@ int sq_destroy(sq_ctx *c) {
         (void)hipFree(s.snap);
         if (s.sA) (void)hipStreamDestroy(s.sA);
         if (s.sB) (void)hipStreamDestroy(s.sB);
-        if (s.evA) (void)hipEventDestroy(s.evA);
         if (s.evC) (void)hipEventDestroy(s.evC);
         if (s.evE) (void)hipEventDestroy(s.evE);
         if (s.evS) (void)hipEventDestroy(s.evS);
+        for (hipEvent_t e : s.evk)
+            if (e) (void)hipEventDestroy(e);
         (void)hipFree(s.stage);
     }
     for (int k = 0; k < 2; ++k) {
@@ -1653,11 +1702,12 @@ int sq_phi4_set_stability(sq_ctx *c, double T, double V) {
     return SQ_OK;
 }
 
-int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, sq_block_op *ops,
-                       int cap, int *nops) {
+int sq_phi4_block_plan(int nz, int ghost, int g, int fuse2, int edge_first, int core_pairs, int rims_b,
+                       sq_block_op *ops, int cap, int *nops) {
     if (!nops || (cap > 0 && !ops)) return fail(SQ_E_ARG, "null argument");
     if (nz < 1 || ghost < 1 || g < 1 || g > ghost || ghost > nz) return fail(SQ_E_ARG, "need 1 <= g <= ghost <= nz");
-    const std::vector<sq_block_op> v = block_plan(nz, ghost, g, fuse2 != 0, edge_first != 0, core_pairs);
+    if (core_pairs < 0) return fail(SQ_E_ARG, "core_pairs must be >= 0");
+    const std::vector<sq_block_op> v = block_plan(nz, ghost, g, fuse2 != 0, edge_first != 0, core_pairs, rims_b != 0);
     *nops = (int)v.size();
     if ((int)v.size() > cap) return fail(SQ_E_ARG, "cap too small: need " + std::to_string(v.size()));
     std::copy(v.begin(), v.end(), ops);

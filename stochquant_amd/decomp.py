@@ -39,19 +39,19 @@ def halo_bytes_per_step(Lx, Ly, dtype_bytes=4):
 
 OP_NAMES = {_lib.SQ_OP_EXCHANGE: "exchange", _lib.SQ_OP_STEP: "step", _lib.SQ_OP_PAIR: "pair",
             _lib.SQ_OP_WAIT_EXCHANGE: "wait_exchange", _lib.SQ_OP_EDGES_DONE: "edges_done",
-            _lib.SQ_OP_WAIT_STAGED: "wait_staged"}
+            _lib.SQ_OP_WAIT_STAGED: "wait_staged", _lib.SQ_OP_SIGNAL: "signal", _lib.SQ_OP_WAIT: "wait"}
 
 
-def block_plan(nz, ghost, g, fuse2=True, edge_first=True, core_pairs=1):
+def block_plan(nz, ghost, g, fuse2=True, edge_first=True, core_pairs=1, rims_b=False):
     """The schedule of one deep-halo block of g <= ghost steps on a slab of nz
-    planes: a list of dicts {op, step, lo, hi, lo2, hi2}."""
+    planes: a list of dicts {op, step, lo, hi, lo2, hi2, stream} (stream "A" or "B")."""
     cap = 64
     ops = (_lib.SqBlockOp * cap)()
     n = ctypes.c_int()
     _lib.call("sq_phi4_block_plan", int(nz), int(ghost), int(g), 1 if fuse2 else 0, 1 if edge_first else 0,
-              int(core_pairs), ops, cap, ctypes.byref(n))
-    return [{"op": OP_NAMES[o.kind], "step": o.step, "lo": o.lo, "hi": o.hi, "lo2": o.lo2, "hi2": o.hi2}
-            for o in ops[:n.value]]
+              int(core_pairs), 1 if rims_b else 0, ops, cap, ctypes.byref(n))
+    return [{"op": OP_NAMES[o.kind], "step": o.step, "lo": o.lo, "hi": o.hi, "lo2": o.lo2, "hi2": o.hi2,
+             "stream": "AB"[o.stream]} for o in ops[:n.value]]
 
 
 def pick_ghost(ms):

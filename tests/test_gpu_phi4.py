@@ -381,11 +381,14 @@ def test_fused_two_step_deep_halo_bitwise(gpu, oracle_mod, monkeypatch, shape, g
         assert np.array_equal(mono, L.download())
 
 
-@pytest.mark.parametrize("core_pairs", ["2", "4", "8"])
-def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs):
-    """K fused core pairs before the exchange wait, their rims after it (the
-    C4 overlap for slow links): RCCL self-exchange and loopback slabs ==
-    the single-slab run, bit for bit, over full and partial blocks."""
+@pytest.mark.parametrize("core_pairs,rims_b", [("0", "0"), ("1", "1"), ("2", "0"), ("2", "1"), ("4", "0"),
+                                                ("4", "1"), ("8", "1")])
+def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs, rims_b):
+    """K fused core pairs before the exchange wait (K = 0: none, the first
+    pair waits for the exchange), their rims after it on stream A or on the
+    exchange stream (the C4 overlap for slow links): RCCL self-exchange, P2P
+    self-exchange and loopback slabs == the single-slab run, bit for bit,
+    over full and partial blocks."""
     from stochquant_amd import unique_id
     shape = (256, 16, 96)
     phi0 = _init(oracle_mod, shape)
@@ -394,10 +397,14 @@ def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, 
         L.step(37)
         mono = L.download()
     monkeypatch.setenv("SQ_CORE_PAIRS", core_pairs)
+    monkeypatch.setenv("SQ_RIMS_B", rims_b)
     monkeypatch.setenv("SQ_GHOST", "16")
     monkeypatch.setenv("SQ_FUSE2", "1")
-    for kw in (dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id()), dict(comm="loopback", nslabs=2)):
+    for kw in (dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id()), dict(comm="loopback", nslabs=2),
+               dict(comm="p2p", nranks=1, rank=0)):
         with _lat(shape, **kw) as L:
+            if kw["comm"] == "p2p":
+                L.p2p_connect([L.p2p_handle()])
             L.upload(phi0)
             for n in (16, 21):
                 L.step(n)

@@ -69,20 +69,51 @@ def _ranges(op):
     return r
 
 
-def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn):
-    """Execute one block's schedule as phi4_block does: consecutive STEP or
-    PAIR ops of one step form a group that reads the latest buffer and writes
-    the other; returns the buffer holding the result."""
-    inb, flip, gstep, gkind = cur, False, -1, None
-    for op in plan:
+def _stream_order(plan, prefer):
+    """A sequential order of the block's ops that respects what the product's
+    two streams guarantee: each stream runs its ops in list order, a WAIT runs
+    after its SIGNAL, WAIT_EXCHANGE / WAIT_STAGED after the exchange.  `prefer`
+    "A" runs stream A whenever it can (the interior as far ahead of the
+    exchange and the rims as the waits allow), "B" the other way round, "list"
+    the list order itself.  A plan that lets one stream read what the other
+    has not written yet then reads NaN (or a stale step) and fails the test."""
+    if prefer == "list":
+        return list(plan)
+    queues = {"A": [op for op in plan if op["stream"] == "A"], "B": [op for op in plan if op["stream"] == "B"]}
+    done, out = set(), []
+
+    def ready(op):
+        k = op["op"]
+        if k in ("wait_exchange", "wait_staged"):
+            return "exchange" in done
+        if k == "wait":
+            return ("signal", op["lo"]) in done
+        return True
+
+    while queues["A"] or queues["B"]:
+        for name in (prefer, "B" if prefer == "A" else "A"):
+            if queues[name] and ready(queues[name][0]):
+                op = queues[name].pop(0)
+                out.append(op)
+                done.add(("signal", op["lo"]) if op["op"] == "signal" else op["op"])
+                break
+        else:
+            raise AssertionError("block plan deadlocks: " + repr([q[0] for q in queues.values() if q]))
+    return out
+
+
+def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn, prefer="list"):
+    """Execute one block's schedule as phi4_block does, in one sequential order
+    of its two streams (_stream_order): a launch group (the STEP / PAIR ops of
+    one first step) reads the buffer the group before it wrote; returns the
+    buffer holding the result."""
+    starts = sorted({op["step"] for op in plan if op["op"] in ("step", "pair")})
+    for op in _stream_order(plan, prefer):
         k = op["op"]
         if k == "exchange":
             _exchange(bufs, cur, nz, G, world, up, dn)
         elif k in ("step", "pair"):
-            if op["step"] != gstep or k != gkind:
-                if flip:
-                    inb ^= 1
-                flip, gstep, gkind = True, op["step"], k
+            inb = cur ^ (starts.index(op["step"]) & 1)
             s = step0 + op["step"]
             for lo, hi in _ranges(op):
                 if k == "step":
@@ -92,11 +123,11 @@ def _run_block(oracle, p, plan, bufs, cur, nz, G, z0, step0, world, up, dn):
                     oracle.phi4_step_range(p, bufs[inb], mid, G, lo - 1, hi + 1, z0, s)
                     oracle.phi4_step_range(p, mid, bufs[inb ^ 1], G, lo, hi, z0, s + 1)
         else:
-            assert k in ("wait_exchange", "edges_done", "wait_staged")
-    return inb ^ 1 if flip else inb
+            assert k in ("wait_exchange", "edges_done", "wait_staged", "signal", "wait")
+    return cur ^ (len(starts) & 1)
 
 
-def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q, core_pairs=1):
+def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q, core_pairs=1, prefer="list", rims_b=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "oracle"))
@@ -127,8 +158,8 @@ def _worker(rank, world, port, steps, fuse2, edge_first, gpad, q, core_pairs=1):
         cur, done = 0, 0
         while done < steps:
             g = min(G, steps - done)
-            plan = block_plan(nz, G, g, fuse2, edge_first, core_pairs)
-            cur = _run_block(oracle, p, plan, bufs, cur, nz, G, z0, done, world, up, dn)
+            plan = block_plan(nz, G, g, fuse2, edge_first, core_pairs, rims_b)
+            cur = _run_block(oracle, p, plan, bufs, cur, nz, G, z0, done, world, up, dn, prefer)
             done += g
         gathered = [None for _ in range(world)]
         dist.all_gather_object(gathered, (z0, G, bufs[cur][G:G + nz].copy()))
@@ -148,25 +179,31 @@ def _monolithic(steps):
     return phi
 
 
-@pytest.mark.parametrize("world,steps,fuse2,edge_first,gpad,core_pairs", [
-    (2, 11, True, True, 4, 1),    # P = 2: both neighbours the same peer; partial last block (11 = 4+4+3)
-    (3, 11, True, True, 4, 1),
-    (2, 9, False, True, 4, 1),    # per-step inner launches
-    (3, 8, True, False, 4, 1),    # edges not first
-    (2, 9, True, True, 8, 1),     # deeper zone: pairs over 2 ghost planes
-    (2, 12, True, True, 2, 1),    # G = 2: blocks of one core/rim step and one edges-first step
-    (3, 10, True, True, 8, 1),    # G = 8 over slabs of 12 planes: rims of 8 planes, no edge split
-    (1, 7, True, True, 4, 1),     # single rank, self-exchange
-    (2, 17, True, True, 8, 2),    # two core pairs ahead of the exchange
-    (2, 19, True, True, 8, 4),    # every pair of the block split into core and rim
-    (3, 11, True, False, 8, 3),   # three core pairs, slabs of 12 planes (the core shrinks to 4)
+@pytest.mark.parametrize("world,steps,fuse2,edge_first,gpad,core_pairs,prefer,rims_b", [
+    (2, 11, True, True, 4, 1, "list", False),  # P = 2: both neighbours one peer; partial last block (4+4+3)
+    (3, 11, True, True, 4, 1, "A", True),      # interior as far ahead as the waits allow
+    (3, 11, True, True, 4, 1, "B", True),      # exchange and rims as far ahead as the waits allow
+    (3, 11, True, True, 4, 1, "A", False),
+    (2, 9, False, True, 4, 1, "A", True),      # per-step inner launches
+    (2, 9, False, True, 4, 0, "B", False),     # ... without a core/rim split
+    (3, 8, True, False, 4, 1, "list", False),  # edges not first
+    (2, 9, True, True, 8, 1, "B", True),       # deeper zone: pairs over 2 ghost planes
+    (2, 12, True, True, 2, 1, "A", False),     # G = 2: blocks of one core/rim step and one edges-first step
+    (3, 10, True, True, 8, 1, "list", True),   # G = 8 over slabs of 12 planes: rims of 8 planes, no edge split
+    (1, 7, True, True, 4, 1, "B", False),      # single rank, self-exchange
+    (2, 13, True, True, 8, 0, "A", False),     # no core/rim split: the first pair waits for the exchange
+    (2, 17, True, True, 8, 2, "A", True),      # two core pairs ahead of the exchange
+    (2, 17, True, True, 8, 2, "B", True),
+    (2, 17, True, True, 8, 2, "B", False),
+    (2, 19, True, True, 8, 4, "A", True),      # every pair of the block split into core and rim
+    (3, 11, True, False, 8, 3, "B", True),     # three core pairs, slabs of 12 planes (the core shrinks to 4)
 ])
-def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, core_pairs, oracle_mod):
+def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, core_pairs, prefer, rims_b, oracle_mod):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, fuse2, edge_first, gpad, q, core_pairs))
-             for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, steps, fuse2, edge_first, gpad, q, core_pairs, prefer,
+                                               rims_b)) for r in range(world)]
     for p in procs:
         p.start()
     ghosts, got = q.get(timeout=240)
@@ -180,41 +217,56 @@ def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, co
 
 
 def test_block_plan_shapes():
-    """The schedule's ranges: fused blocks pair every step --
-    a core pair overlapping the exchange, a rim pair after it, pairs over the
-    shrinking ghost range, the last pair edges first; unfused blocks split
-    step 0 into core and rim and run the rest one step per launch."""
+    """The schedule's ranges and streams: fused blocks pair
+    every step -- a core pair on stream A overlapping the exchange, the rim pair
+    on stream B right behind the exchange, stream A waiting for the rims before
+    the pairs over the shrinking ghost range, the last pair edges first;
+    unfused blocks split step 0 into core (A) and rim (B) and run the rest one
+    step per launch on A."""
     from stochquant_amd.decomp import block_plan
+
+    def sig(ops):
+        return [(o["op"], o["step"], o["lo"], o["hi"], o["lo2"], o["hi2"], o["stream"]) for o in ops]
+
     ops = block_plan(64, 16, 16)
-    assert [o["op"] for o in ops[:4]] == ["exchange", "pair", "wait_exchange", "pair"]
-    assert (ops[1]["step"], ops[1]["lo"], ops[1]["hi"]) == (0, 2, 62)
-    assert (ops[3]["lo"], ops[3]["hi"], ops[3]["lo2"], ops[3]["hi2"]) == (-14, 2, 62, 78)
+    assert sig(ops[:4]) == [
+        ("exchange", 0, 0, 0, 0, 0, "B"), ("pair", 0, 2, 62, 0, 0, "A"), ("wait_exchange", 0, 0, 0, 0, 0, "A"),
+        ("pair", 0, -14, 2, 62, 78, "A")]
+    assert sig(block_plan(64, 16, 16, rims_b=True)[:6]) == [
+        ("exchange", 0, 0, 0, 0, 0, "B"), ("pair", 0, 2, 62, 0, 0, "A"), ("wait_exchange", 0, 0, 0, 0, 0, "B"),
+        ("pair", 0, -14, 2, 62, 78, "B"), ("signal", 0, 15, 0, 0, 0, "B"), ("wait", 0, 15, 0, 0, 0, "A")]
+    assert sig(block_plan(64, 16, 16, core_pairs=0)[:3]) == [
+        ("exchange", 0, 0, 0, 0, 0, "B"), ("wait_exchange", 0, 0, 0, 0, 0, "A"), ("pair", 0, -14, 78, 0, 0, "A")]
     inner = [o for o in ops[4:] if o["op"] == "pair" and 0 < o["step"] < 14]
-    assert [(o["step"], o["lo"], o["hi"]) for o in inner] == [(s, -(14 - s), 64 + 14 - s) for s in range(2, 14, 2)]
+    assert [(o["step"], o["lo"], o["hi"], o["stream"]) for o in inner] == [
+        (s, -(14 - s), 64 + 14 - s, "A") for s in range(2, 14, 2)]
     tail = [o for o in ops if o["step"] == 14]
-    assert [(o["op"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in tail] == [
-        ("pair", 0, 16, 48, 64), ("edges_done", 0, 0, 0, 0), ("pair", 16, 48, 0, 0)]
+    assert sig(tail) == [("pair", 14, 0, 16, 48, 64, "A"), ("edges_done", 14, 0, 0, 0, 0, "A"),
+                         ("pair", 14, 16, 48, 0, 0, "A")]
     # odd g: the last step single, edges first
     ops = block_plan(40, 4, 3)
-    assert [(o["op"], o["step"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in ops] == [
-        ("exchange", 0, 0, 0, 0, 0), ("pair", 0, 2, 38, 0, 0), ("wait_exchange", 0, 0, 0, 0, 0),
-        ("pair", 0, -1, 2, 38, 41), ("step", 2, 0, 4, 36, 40), ("edges_done", 2, 0, 0, 0, 0),
-        ("step", 2, 4, 36, 0, 0)]
-    # K core pairs run ahead of the exchange; their rims follow it, then the rest
-    ops = block_plan(64, 8, 8, core_pairs=2)
-    assert [(o["op"], o["step"], o["lo"], o["hi"], o["lo2"], o["hi2"]) for o in ops] == [
-        ("exchange", 0, 1, 0, 0, 0), ("pair", 0, 2, 62, 0, 0), ("wait_staged", 0, 0, 0, 0, 0),
-        ("pair", 2, 4, 60, 0, 0),
-        ("wait_exchange", 0, 0, 0, 0, 0), ("pair", 0, -6, 2, 62, 70), ("pair", 2, -4, 4, 60, 68),
-        ("pair", 4, -2, 66, 0, 0), ("pair", 6, 0, 8, 56, 64), ("edges_done", 6, 0, 0, 0, 0),
-        ("pair", 6, 8, 56, 0, 0)]
-    ops = block_plan(64, 8, 8, core_pairs=4)   # every pair split: the last rims are the edges
+    assert sig(ops) == [
+        ("exchange", 0, 0, 0, 0, 0, "B"), ("pair", 0, 2, 38, 0, 0, "A"), ("wait_exchange", 0, 0, 0, 0, 0, "A"),
+        ("pair", 0, -1, 2, 38, 41, "A"),
+        ("step", 2, 0, 4, 36, 40, "A"), ("edges_done", 2, 0, 0, 0, 0, "A"), ("step", 2, 4, 36, 0, 0, "A")]
+    # K core pairs run ahead of the exchange on A (the second after the staged
+    # copy); their rims follow the exchange on B, rim j after core j-1
+    ops = block_plan(64, 8, 8, core_pairs=2, rims_b=True)
+    assert sig(ops) == [
+        ("exchange", 0, 1, 0, 0, 0, "B"), ("pair", 0, 2, 62, 0, 0, "A"), ("signal", 0, 0, 0, 0, 0, "A"),
+        ("wait_staged", 0, 0, 0, 0, 0, "A"), ("pair", 2, 4, 60, 0, 0, "A"),
+        ("wait_exchange", 0, 0, 0, 0, 0, "B"), ("pair", 0, -6, 2, 62, 70, "B"), ("wait", 2, 0, 0, 0, 0, "B"),
+        ("pair", 2, -4, 4, 60, 68, "B"), ("signal", 0, 15, 0, 0, 0, "B"), ("wait", 0, 15, 0, 0, 0, "A"),
+        ("pair", 4, -2, 66, 0, 0, "A"), ("pair", 6, 0, 8, 56, 64, "A"), ("edges_done", 6, 0, 0, 0, 0, "A"),
+        ("pair", 6, 8, 56, 0, 0, "A")]
+    ops = block_plan(64, 8, 8, core_pairs=4, rims_b=True)   # every pair split: the last rims are the edges
     assert [o["op"] for o in ops].count("pair") == 8 and ops[-1]["op"] == "edges_done"
-    assert (ops[-2]["lo"], ops[-2]["hi"], ops[-2]["lo2"], ops[-2]["hi2"]) == (0, 8, 56, 64)
+    last_rim = [o for o in ops if o["op"] == "pair" and o["stream"] == "B"][-1]
+    assert (last_rim["lo"], last_rim["hi"], last_rim["lo2"], last_rim["hi2"]) == (0, 8, 56, 64)
     # unfused: every step 1..g-1 covered once, the last one ghost-free
     ops = block_plan(12, 4, 3, fuse2=False, edge_first=False)
-    steps = [(o["step"], o["lo"], o["hi"]) for o in ops if o["op"] == "step"]
-    assert steps == [(0, 1, 11), (0, -2, 1), (1, -1, 13), (2, 0, 12)]
+    steps = [(o["step"], o["lo"], o["hi"], o["stream"]) for o in ops if o["op"] == "step"]
+    assert steps == [(0, 1, 11, "A"), (0, -2, 1, "A"), (1, -1, 13, "A"), (2, 0, 12, "A")]
     assert ops[-1]["op"] == "edges_done"
 
 
