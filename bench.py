@@ -238,9 +238,10 @@ def main():
             dist.barrier()
 
     if slab_path:
-        # setup: the timed trial blocks of the multi-rank slab path, 3 x G steps per
-        # candidate (G, core pairs) in {(4,1), (8,1), (16,1), (16,2), (16,4)}
-        lat.step(180)
+        # setup: the timed trial blocks of the multi-rank slab path (one call long
+        # enough for all of them), 3 x G steps per candidate (G, core pairs, rims)
+        # in {(4,1,A), (8,1,A), (16,1,A), (16,0), (16,2|4,A|B)}: 324 steps
+        lat.step(400)
     # clock settle: untimed batches until settle_ms have passed on rank 0 (every
     # rank runs the same batches: the slab exchanges must pair up)
     settle_steps = 0
@@ -331,6 +332,7 @@ def main():
                 "per_gpu": [L, L, lat.nz_local],
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
                 "ghost_depth": lat.ghost[0] if slab_path else None,
+                "block_schedule": lat.schedule if slab_path else None,
                 "parallelism": "single GPU, one stream" if not slab_path else
                                f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else 'rccl'}), halo exchange on "
                                f"stream B, interior on stream A",

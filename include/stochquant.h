@@ -174,6 +174,11 @@ int sq_phi4_kernel(sq_ctx *ctx, char *name, size_t cap);
  * first sq_step / sq_run_frame calls) and the depth allocated; 0, 0 for a
  * single periodic slab. */
 int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
+/* The rest of a slab decomposition's block schedule: core pairs ahead of
+ * each exchange, rims on the exchange stream (1) or the interior stream (0),
+ * and whether the timed trials chose them (1) or they are the defaults /
+ * SQ_CORE_PAIRS / SQ_RIMS_B (0).  Single periodic slab: 0, 0, 0. */
+int sq_phi4_schedule(sq_ctx *ctx, int *core_pairs, int *rims_b, int *tuned);
 /* The launch schedule of one deep-halo block (pure host logic, no device
  * needed; the product's phi4_block executes exactly this list): a slab of nz
  * planes with a ghost zone of `ghost` planes (the exchange depth G) running

@@ -1675,6 +1675,16 @@ int sq_phi4_ghost(sq_ctx *c, int *active, int *allocated) {
     return SQ_OK;
 }
 
+int sq_phi4_schedule(sq_ctx *c, int *core_pairs, int *rims_b, int *tuned) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    const bool slab = c->p.comm != SQ_COMM_NONE;
+    if (core_pairs) *core_pairs = slab ? c->core_pairs : 0;
+    if (rims_b) *rims_b = slab && c->rims_b ? 1 : 0;
+    if (tuned) *tuned = c->g_tuned ? 1 : 0;
+    return SQ_OK;
+}
+
 int sq_phi4_stability(sq_ctx *c, double state[2], int *fired_step, float *M, float *D, float *A, int n) {
     if (!c) return fail(SQ_E_ARG, "null context");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");

@@ -271,6 +271,13 @@ class Phi4Lattice(_Ctx):
         _lib.call("sq_phi4_ghost", self._h, ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
 
+    @property
+    def schedule(self):
+        """{"ghost", "core_pairs", "rims_b", "tuned"} of a slab decomposition's block schedule."""
+        k, b, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.call("sq_phi4_schedule", self._h, ctypes.byref(k), ctypes.byref(b), ctypes.byref(t))
+        return {"ghost": self.ghost[0], "core_pairs": k.value, "rims_b": bool(b.value), "tuned": bool(t.value)}
+
     def save(self, path):
         """Binary checkpoint: <path> (.npy float32 (nz, Ly, Lx)) + <path>.json (step, dtau, seed, z0)."""
         _lib.call("sq_save_field", self._h, os.fsencode(path))

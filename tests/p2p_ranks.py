@@ -37,6 +37,7 @@ def rank_main(conn, rank, nranks, shape, kw, env, script):
                 out["correlator"] = lat.correlator(arg)
             elif op == "ghost":
                 out["ghost"] = lat.ghost
+                out["schedule"] = lat.schedule
             else:
                 raise ValueError(op)
         out["step_counter"] = lat.step_counter

@@ -143,15 +143,16 @@ def test_p2p_ranks_bitwise_vs_single_slab(gpu, nranks, shape, steps, env):
 
 
 def test_p2p_ghost_trials_agree_across_ranks(gpu):
-    """Multi-rank P2P contexts time G in {4, 8, 16} (and core pairs 2, 4)
-    and max-reduce the trial times over peer memory: every rank keeps the same
-    depth, and the trial steps are ordinary steps."""
+    """Multi-rank P2P contexts time G in {4, 8, 16} and the core-pair / rim
+    schedules and max-reduce the trial times over peer memory: every rank keeps
+    the same schedule, and the trial steps are ordinary steps."""
     shape = (256, 16, 128)
     phi0 = _field0(shape)
-    script = [("upload", phi0), ("step", 200), ("ghost", None), ("field", None)]
+    script = [("upload", phi0), ("step", 340), ("ghost", None), ("field", None)]
     mono = _mono(shape, KW, script)
     outs = run_ranks(2, shape, KW, script)
     assert outs[0]["ghost"] == outs[1]["ghost"] and outs[0]["ghost"][0] in (4, 8, 16)
+    assert outs[0]["schedule"] == outs[1]["schedule"] and outs[0]["schedule"]["tuned"]
     assert np.array_equal(_assemble(outs), mono["field"][0])
 
 

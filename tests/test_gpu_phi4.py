@@ -543,7 +543,7 @@ def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
     monkeypatch.setenv("SQ_GHOST_AUTO", "1")
     shape = (256, 8, 128)
     phi0 = _init(oracle_mod, shape)
-    steps = 200            # >= 3*(4+8+16+16+16) = 180 trial steps, then 20 more
+    steps = 340            # >= 3*(4+8+16) + 5*3*16 = 324 trial steps, then 16 more
     with _lat(shape) as L:
         L.upload(phi0)
         L.step(steps)
@@ -555,6 +555,8 @@ def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
         L.step(steps)
         act, alloc = L.ghost
         assert alloc == 16 and act in (4, 8, 16)
+        sch = L.schedule
+        assert sch["tuned"] and sch["core_pairs"] in (0, 1, 2, 4)
         assert L.step_counter == steps
         assert np.array_equal(L.download(), mono)
 
