@@ -45,19 +45,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t plane_rsrc(const float *base, 
     return __builtin_amdgcn_make_buffer_rsrc((void *)(base + (size_t)padded * plane), (short)0,
                                              (int)pbytes, 0x00020000);
 }
+// soff: a wave-uniform byte offset added by the buffer unit (the plane of a
+// whole-buffer descriptor, tb2 kernel)
 template <int LAUX = 0>
-__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LAUX);
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
+    const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, LAUX);
     return make_float4(v.x, v.y, v.z, v.w);
 }
 template <int AUX = 0>
-__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v, uint32_t soff = 0) {
     const f32x4v w = {v.x, v.y, v.z, v.w};
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, off, soff, AUX);
 }
 template <int LAUX = 0>
-__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, LAUX));
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff = 0) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, soff, LAUX));
 }
 
 __device__ __forceinline__ int padded_index(const Phi4StepArgs &A, int zl) {
@@ -584,6 +586,7 @@ struct TbIn {
 struct TbCtx {
     size_t plane;
     uint32_t pbytes, qplane;
+    __amdgpu_buffer_rsrc_t rin, rout;  // WH: one descriptor over each whole padded buffer
     // byte offsets in a plane and the Philox quad offset.  Row waves: voff
     // their row, vm / vp its y-neighbours, vex the site just outside the
     // segment (lane 0 left, lane 63 right).  x-halo wave lanes (sharing the
@@ -608,22 +611,36 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
 // One plane of the march.  Row waves: I0 (p-1), I1 (p), I2 (p+1, loaded
 // here); T0 (p-2), T1 (p-1), T2 (p, computed here).  The x-halo wave: the
 // centres of its sites at the same planes in row.x.
-template <bool NZ, bool WIDE, bool FR>
+// J = (p - (z0 - 1)) % 3, the unroll position: plane p's LDS slot (any
+// block-wide bijection of the three planes in flight works, and this one is a
+// compile-time constant).  WH: the padded buffers fit one 32-bit descriptor
+// each, and the plane is the buffer unit's scalar offset (one s_mul per plane
+// instead of the 64-bit descriptor base arithmetic).
+template <bool NZ, bool WIDE, bool FR, bool WH, int J>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
                                          FrameAcc &f2) {
-    const __amdgpu_buffer_rsrc_t rs = plane_rsrc(A.in, tb_pidx(A, p + 1), K.plane, K.pbytes);
-    // S > 1: plane p's values at the segment's outer x-neighbours (lane 0 x0-1,
-    // lane 63 x0+256) and at the x-halo sites' in-plane neighbours are loaded
-    // in the iteration that uses them, like plane p+1 itself
-    const __amdgpu_buffer_rsrc_t rc = plane_rsrc(A.in, tb_pidx(A, p), K.plane, K.pbytes);
+    constexpr int sl = J, sp = (J + 2) % 3;  // slots of planes p and p-1
+    __amdgpu_buffer_rsrc_t rs, rc;
+    uint32_t ss = 0, sc = 0;
+    if constexpr (WH) {
+        rs = rc = K.rin;
+        ss = (uint32_t)tb_pidx(A, p + 1) * K.pbytes;
+        sc = (uint32_t)tb_pidx(A, p) * K.pbytes;
+    } else {
+        rs = plane_rsrc(A.in, tb_pidx(A, p + 1), K.plane, K.pbytes);
+        // S > 1: plane p's values at the segment's outer x-neighbours (lane 0 x0-1,
+        // lane 63 x0+256) and at the x-halo sites' in-plane neighbours are loaded
+        // in the iteration that uses them, like plane p+1 itself
+        rc = plane_rsrc(A.in, tb_pidx(A, p), K.plane, K.pbytes);
+    }
     if (!WIDE || K.w < kTbWaves) {
-        I2.row = bload4(rs, K.voff);
-        I2.hm = bload4(rs, K.vm);
-        I2.hp = bload4(rs, K.vp);
+        I2.row = bload4(rs, K.voff, ss);
+        I2.hm = bload4(rs, K.vm, ss);
+        I2.hp = bload4(rs, K.vp, ss);
         float ex = 0.f;
-        if constexpr (WIDE) ex = bload1(rc, K.vex);
+        if constexpr (WIDE) ex = bload1(rc, K.vex, sc);
         const f32x4n xa = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
         float lft = from_left_lane(I1.row.w), rgt = from_right_lane(I1.row.x);
         if constexpr (WIDE) {
@@ -632,22 +649,21 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         }
         T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0);
         if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa);
-        const int sl = (p % 3 + 3) % 3;  // p < 0 in the first chunk (and in ghost zones)
         lds[sl][K.w][K.lane] = T2;
     } else {
         // the x-halo wave: step s at its 16 sites of plane p
-        I2.row.x = bload1(rs, K.voff);
-        const float xm = bload1(rc, K.vex), xp = bload1(rc, K.vx2), ym = bload1(rc, K.vm), yp = bload1(rc, K.vp);
+        I2.row.x = bload1(rs, K.voff, ss);
+        const float xm = bload1(rc, K.vex, sc), xp = bload1(rc, K.vx2, sc), ym = bload1(rc, K.vm, sc),
+                    yp = bload1(rc, K.vp, sc);
         const f32x4n n = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
         // lanes 0..7 hold x0-1 (component 3 of its quad), 8..15 x0+256 (component 0)
         const float xi = K.lane >= 8 ? n.a : n.d;
         const float t = tb_site(I1.row.x, xm, xp, ym, yp, I0.row.x, I2.row.x, xi, A, NZ);
-        if (K.lane < 16) tx[(p % 3 + 3) % 3][(K.lane & 7) + 1][K.lane >> 3] = t;
+        if (K.lane < 16) tx[sl][(K.lane & 7) + 1][K.lane >> 3] = t;
     }
     __syncthreads();
     if (K.outw && p > K.z0) {
         const f32x4n xb = tb_noise<NZ>(A, p - 1, K.qoff, K.qplane, K.slo1, K.shi1);
-        const int sp = ((p + 2) % 3 + 3) % 3;  // slot of plane p-1
         const float4 up = lds[sp][K.w - 1][K.lane], dn = lds[sp][K.w + 1][K.lane];
         float lft = from_left_lane(T1.w), rgt = from_right_lane(T1.x);
         if constexpr (WIDE) {
@@ -657,8 +673,12 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         // step s+1 reads step s's guarded output: always finite
         const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true);
         if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb);
-        const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
-        bstore4<17>(ws, K.voff, o);
+        if constexpr (WH) {
+            bstore4<17>(K.rout, K.voff, o, (uint32_t)(p - 1 + A.gz) * K.pbytes);
+        } else {
+            const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
+            bstore4<17>(ws, K.voff, o);
+        }
     }
 }
 
@@ -667,7 +687,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 // 256-wide rows: 65 VGPRs, two 10-wave blocks per CU.  A 64-VGPR budget
 // (three blocks per CU) measured slower at every z-chunk
 // (profiles/r01/fuse2_sweep.log).
-template <bool NZ, bool WIDE, int WPE, bool FR>
+template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A) {
     const int nb = gridDim.x, b = blockIdx.x;
@@ -689,6 +709,11 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     K.plane = (size_t)Lx * (size_t)Ly;
     K.pbytes = (uint32_t)(K.plane * sizeof(float));
     K.qplane = (uint32_t)(K.plane >> 2);
+    if constexpr (WH) {
+        const int nbytes = (int)((uint32_t)(A.nz + 2 * A.gz) * K.pbytes);  // < 2^31 (phi4_tb2_launch)
+        K.rin = __builtin_amdgcn_make_buffer_rsrc((void *)A.in, (short)0, nbytes, 0x00020000);
+        K.rout = __builtin_amdgcn_make_buffer_rsrc((void *)A.out, (short)0, nbytes, 0x00020000);
+    }
     const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
     K.slo = (uint32_t)s0;
     K.shi = (uint32_t)(s0 >> 32);
@@ -740,11 +765,11 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     FrameAcc f1 = frame_acc(), f2 = frame_acc();  // steps s and s+1
     // three-plane queues unrolled three ways so no rotation moves are emitted
     for (int p = K.z0 - 1; p <= z1; p += 3) {
-        tb_plane<NZ, WIDE, FR>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
         if (p + 1 > z1) break;
-        tb_plane<NZ, WIDE, FR>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
         if (p + 2 > z1) break;
-        tb_plane<NZ, WIDE, FR>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
     }
     if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
         __shared__ uint64_t sk[kTbWaves + 1];
@@ -962,7 +987,11 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     static const int wpe = getenv("SQ_TB2_WPE") ? atoi(getenv("SQ_TB2_WPE")) : 6;
     const bool fr = a.flag != nullptr;
     const void *fn;
-#define SQ_TB2(N, W, E) (fr ? (const void *)&phi4_tb2_kernel<N, W, E, true> : (const void *)&phi4_tb2_kernel<N, W, E, false>)
+    // one 32-bit (signed, < 2^31 B) descriptor per padded buffer when it fits
+    const bool wh = (long long)(a.nz + 2 * a.gz) * a.Lx * a.Ly * 4 < (1ll << 31);
+#define SQ_TB2F(N, W, E, F) (wh ? (const void *)&phi4_tb2_kernel<N, W, E, F, true> \
+                             : (const void *)&phi4_tb2_kernel<N, W, E, F, false>)
+#define SQ_TB2(N, W, E) (fr ? SQ_TB2F(N, W, E, true) : SQ_TB2F(N, W, E, false))
     if (wide && wpe == 6)
         fn = nz ? SQ_TB2(true, true, 6) : SQ_TB2(false, true, 6);
     else if (wide)
@@ -970,6 +999,7 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     else
         fn = nz ? SQ_TB2(true, false, 1) : SQ_TB2(false, false, 1);
 #undef SQ_TB2
+#undef SQ_TB2F
     Phi4StepArgs q = a;
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
