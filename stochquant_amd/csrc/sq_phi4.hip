@@ -559,13 +559,14 @@ __device__ __forceinline__ int tb_pidx(const Phi4StepArgs &A, int zl) {
     return zl + A.gz;
 }
 
+// qz: the Philox quad index of the plane's first site (global z * plane / 4)
 template <bool NZ>
-__device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, int zl, uint32_t qoff, uint32_t qplane,
-                                           uint32_t slo, uint32_t shi) {
+__device__ __forceinline__ f32x4n tb_noise(const Phi4StepArgs &A, uint32_t qz, uint32_t qoff, uint32_t slo,
+                                           uint32_t shi) {
     f32x4n xi;
     if constexpr (NZ) {
         u32x4 c[1];
-        c[0] = u32x4{(uint32_t)global_z(A, zl) * qplane + qoff, kStreamField << 24, slo, shi};
+        c[0] = u32x4{qz + qoff, kStreamField << 24, slo, shi};
         philox_field<1>(c, A.k0, A.k1);
         box_muller_q(c[0].x, c[0].y, xi.a, xi.b);  // scaled by 1/sqrt(2 ln 2); A.sigq carries the factor
         box_muller_q(c[0].z, c[0].w, xi.c, xi.d);
@@ -593,8 +594,19 @@ struct TbCtx {
     // registers): voff the site, vm / vp its y-neighbours, vex / vx2 its x-1 / x+1.
     uint32_t voff, vm, vp, vex, vx2, qoff;
     uint32_t slo, shi, slo1, shi1;
+    uint32_t qwrap;      // Lz_global * plane / 4: where the Philox quad base wraps
+    int swrap_at;        // WH, periodic: the plane p at which plane p+1's input wraps to local 0
     int z0, w, lane;
     bool outw;
+};
+
+// Wave-uniform per-plane scalars carried through the march instead of being
+// recomputed from p every plane (the kernel is issue-bound, scalar
+// instructions included): the byte offsets of planes p+1 and p in the padded
+// input (WH) and the Philox quad bases of planes p (step s) and p-1 (step s+1).
+struct TbRun {
+    uint32_t snext, scur;
+    uint32_t qz, qzm;
 };
 
 __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym, float yp, float zm, float zp,
@@ -617,7 +629,7 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
 // each, and the plane is the buffer unit's scalar offset (one s_mul per plane
 // instead of the 64-bit descriptor base arithmetic).
 template <bool NZ, bool WIDE, bool FR, bool WH, int J>
-__device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, int p, const TbIn &I0,
+__device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, TbRun &R, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
                                          FrameAcc &f2) {
@@ -626,8 +638,8 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
     uint32_t ss = 0, sc = 0;
     if constexpr (WH) {
         rs = rc = K.rin;
-        ss = (uint32_t)tb_pidx(A, p + 1) * K.pbytes;
-        sc = (uint32_t)tb_pidx(A, p) * K.pbytes;
+        ss = R.snext;
+        sc = R.scur;
     } else {
         rs = plane_rsrc(A.in, tb_pidx(A, p + 1), K.plane, K.pbytes);
         // S > 1: plane p's values at the segment's outer x-neighbours (lane 0 x0-1,
@@ -641,7 +653,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         I2.hp = bload4(rs, K.vp, ss);
         float ex = 0.f;
         if constexpr (WIDE) ex = bload1(rc, K.vex, sc);
-        const f32x4n xa = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
+        const f32x4n xa = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
         float lft = from_left_lane(I1.row.w), rgt = from_right_lane(I1.row.x);
         if constexpr (WIDE) {
             if (K.lane == 0) lft = ex;
@@ -655,7 +667,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         I2.row.x = bload1(rs, K.voff, ss);
         const float xm = bload1(rc, K.vex, sc), xp = bload1(rc, K.vx2, sc), ym = bload1(rc, K.vm, sc),
                     yp = bload1(rc, K.vp, sc);
-        const f32x4n n = tb_noise<NZ>(A, p, K.qoff, K.qplane, K.slo, K.shi);
+        const f32x4n n = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
         // lanes 0..7 hold x0-1 (component 3 of its quad), 8..15 x0+256 (component 0)
         const float xi = K.lane >= 8 ? n.a : n.d;
         const float t = tb_site(I1.row.x, xm, xp, ym, yp, I0.row.x, I2.row.x, xi, A, NZ);
@@ -663,7 +675,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
     }
     __syncthreads();
     if (K.outw && p > K.z0) {
-        const f32x4n xb = tb_noise<NZ>(A, p - 1, K.qoff, K.qplane, K.slo1, K.shi1);
+        const f32x4n xb = tb_noise<NZ>(A, R.qzm, K.qoff, K.slo1, K.shi1);
         const float4 up = lds[sp][K.w - 1][K.lane], dn = lds[sp][K.w + 1][K.lane];
         float lft = from_left_lane(T1.w), rgt = from_right_lane(T1.x);
         if constexpr (WIDE) {
@@ -679,6 +691,14 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
             bstore4<17>(ws, K.voff, o);
         }
+    }
+    // advance to plane p+1
+    R.qzm = R.qz;
+    const uint32_t q = R.qz + K.qplane;
+    R.qz = q == K.qwrap ? 0u : q;
+    if constexpr (WH) {
+        R.scur = R.snext;
+        R.snext = p == K.swrap_at ? (uint32_t)A.gz * K.pbytes : R.snext + K.pbytes;
     }
 }
 
@@ -714,6 +734,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         K.rin = __builtin_amdgcn_make_buffer_rsrc((void *)A.in, (short)0, nbytes, 0x00020000);
         K.rout = __builtin_amdgcn_make_buffer_rsrc((void *)A.out, (short)0, nbytes, 0x00020000);
     }
+    K.qwrap = (uint32_t)A.Lzg * K.qplane;  // < 2^32 quads (create_phi4)
+    // periodic: plane p+1 = nz is local plane 0 (tb_pidx); p never reaches it otherwise
+    K.swrap_at = A.periodic ? A.nz - 2 : INT_MIN;  // slabs: p < 0 in ghost zones, never INT_MIN
     const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
     K.slo = (uint32_t)s0;
     K.shi = (uint32_t)(s0 >> 32);
@@ -763,13 +786,18 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     }
     float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
     FrameAcc f1 = frame_acc(), f2 = frame_acc();  // steps s and s+1
+    TbRun R;
+    R.scur = (uint32_t)tb_pidx(A, K.z0 - 1) * K.pbytes;
+    R.snext = (uint32_t)tb_pidx(A, K.z0) * K.pbytes;
+    R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
+    R.qzm = 0;  // plane z0-2: no step s+1 output there
     // three-plane queues unrolled three ways so no rotation moves are emitted
     for (int p = K.z0 - 1; p <= z1; p += 3) {
-        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
         if (p + 1 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
         if (p + 2 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
     }
     if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
         __shared__ uint64_t sk[kTbWaves + 1];
