@@ -36,6 +36,17 @@ __device__ __forceinline__ float from_left_lane(float v) {  // lane i <- lane i-
 __device__ __forceinline__ float from_right_lane(float v) {  // lane i <- lane i+1 (mod 64)
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x134, 0xF, 0xF, true));
 }
+// Lane i <- lane i-1 and lane 0 <- edge (DPP wave_shr:1 with bound_ctrl off:
+// the lane without a source keeps the old value, so no v_cndmask), and
+// lane i <- lane i+1, lane 63 <- edge (wave_shl:1).
+__device__ __forceinline__ float from_left_lane_or(float v, float edge) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge),
+                                                                 __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float from_right_lane_or(float v, float edge) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, edge),
+                                                                 __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+}
 
 // Buffer descriptor over ONE plane: the base moves by scalar arithmetic per
 // plane and every per-lane offset (row within the plane) is loop-invariant,
@@ -106,16 +117,23 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // (create_phi4 bounds the drift), never as NaN, so one max3 / max / compare
 // decides whether the guard has anything to do and the 8-instruction guard
 // runs only in waves where some lane does (bit-identical either way).
+// m2v: {m2, m2} (a VOP3P operation reads one scalar operand, and lam6 is the
+// one: the tb2 kernel pins the pair in VGPRs once instead of per update).
 template <bool NZ>
 __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, float4 up, float4 dn,
                                                float4 zm, float4 zp, const f32x4n &xi,
-                                               const Phi4StepArgs &A, bool fin) {
+                                               const Phi4StepArgs &A, bool fin, f32x2 m2v) {
     const f32x2 c0 = {c.x, c.y}, c1 = {c.z, c.w};
-    const f32x2 x0 = {lft + c.y, c.x + c.z}, x1 = {c.y + c.w, c.z + rgt};
+    // c.x + c.z and c.y + c.w as two single adds: formed as one v_pk_add they
+    // share a register pair and take two v_mov to reach x0 / x1
+    float s02, s13;
+    asm("v_add_f32 %0, %1, %2" : "=v"(s02) : "v"(c.x), "v"(c.z));
+    asm("v_add_f32 %0, %1, %2" : "=v"(s13) : "v"(c.y), "v"(c.w));
+    const f32x2 x0 = {lft + c.y, s02}, x1 = {s13, c.z + rgt};
     const f32x2 y0 = f32x2{up.x, up.y} + f32x2{dn.x, dn.y}, y1 = f32x2{up.z, up.w} + f32x2{dn.z, dn.w};
     const f32x2 z0 = f32x2{zm.x, zm.y} + f32x2{zp.x, zp.y}, z1 = f32x2{zm.z, zm.w} + f32x2{zp.z, zp.w};
     const f32x2 nb0 = (x0 + y0) + z0, nb1 = (x1 + y1) + z1;
-    const f32x2 m6 = {-6.0f, -6.0f}, l6 = {A.lam6, A.lam6}, m2 = {A.m2, A.m2}, h = {A.h, A.h};
+    const f32x2 m6 = {-6.0f, -6.0f}, l6 = {A.lam6, A.lam6}, m2 = m2v, h = {A.h, A.h};
     const f32x2 lap0 = __builtin_elementwise_fma(m6, c0, nb0), lap1 = __builtin_elementwise_fma(m6, c1, nb1);
     const f32x2 g0 = __builtin_elementwise_fma(l6, c0 * c0, m2), g1 = __builtin_elementwise_fma(l6, c1 * c1, m2);
     const f32x2 d0 = __builtin_elementwise_fma(-c0, g0, lap0), d1 = __builtin_elementwise_fma(-c1, g1, lap1);
@@ -221,11 +239,11 @@ __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_re
 
 template <int R>
 __device__ __forceinline__ void philox_field(u32x4 (&c)[R], uint32_t k0, uint32_t k1) {
-    const uint32_t cy = uni(c[0].y), cz = uni(c[0].z), cw = uni(c[0].w);
+    const uint32_t cy = c[0].y, cz = c[0].z, cw = c[0].w;  // uniform already (kernel arguments)
     // round 0
     const uint64_t p1u = (uint64_t)kPhiloxM1 * cz;
     const uint32_t u0 = uni((uint32_t)(p1u >> 32) ^ cy ^ k0), u1 = uni((uint32_t)p1u);
-    const uint32_t a0 = uni(cw ^ k1);
+    const uint32_t a0 = cw ^ k1;
     uint32_t n2[R], n3[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -403,7 +421,8 @@ __device__ __forceinline__ void plane_compute(const Phi4StepArgs &A, const Lane<
             }
             float4 o;
             if constexpr (PK) {
-                o = site_update4<NZ>(cc, lft, rgt, up, dn, P.row[k], N.row[k], xi[k], A, A.fin != 0);
+                o = site_update4<NZ>(cc, lft, rgt, up, dn, P.row[k], N.row[k], xi[k], A, A.fin != 0,
+                                     f32x2{A.m2, A.m2});
             } else {
                 o.x = site_update<NZ>(cc.x, lft, cc.y, up.x, dn.x, P.row[k].x, N.row[k].x, xi[k].a, A);
                 o.y = site_update<NZ>(cc.y, cc.x, cc.z, up.y, dn.y, P.row[k].y, N.row[k].y, xi[k].b, A);
@@ -595,6 +614,7 @@ struct TbCtx {
     uint32_t voff, vm, vp, vex, vx2, qoff;
     uint32_t slo, shi, slo1, shi1;
     uint32_t qwrap;      // Lz_global * plane / 4: where the Philox quad base wraps
+    f32x2 m2v;           // {m2, m2}, pinned in VGPRs (site_update4)
     int swrap_at;        // WH, periodic: the plane p at which plane p+1's input wraps to local 0
     int z0, w, lane;
     bool outw;
@@ -654,12 +674,15 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         float ex = 0.f;
         if constexpr (WIDE) ex = bload1(rc, K.vex, sc);
         const f32x4n xa = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
-        float lft = from_left_lane(I1.row.w), rgt = from_right_lane(I1.row.x);
+        float lft, rgt;
         if constexpr (WIDE) {
-            if (K.lane == 0) lft = ex;
-            if (K.lane == 63) rgt = ex;
+            lft = from_left_lane_or(I1.row.w, ex);
+            rgt = from_right_lane_or(I1.row.x, ex);
+        } else {
+            lft = from_left_lane(I1.row.w);
+            rgt = from_right_lane(I1.row.x);
         }
-        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0);
+        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v);
         if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa);
         lds[sl][K.w][K.lane] = T2;
     } else {
@@ -677,13 +700,17 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
     if (K.outw && p > K.z0) {
         const f32x4n xb = tb_noise<NZ>(A, R.qzm, K.qoff, K.slo1, K.shi1);
         const float4 up = lds[sp][K.w - 1][K.lane], dn = lds[sp][K.w + 1][K.lane];
-        float lft = from_left_lane(T1.w), rgt = from_right_lane(T1.x);
+        float lft, rgt;
         if constexpr (WIDE) {
-            if (K.lane == 0) lft = tx[sp][K.w][0];
-            if (K.lane == 63) rgt = tx[sp][K.w][1];
+            const float2 e = *reinterpret_cast<const float2 *>(&tx[sp][K.w][0]);  // one broadcast LDS read
+            lft = from_left_lane_or(T1.w, e.x);
+            rgt = from_right_lane_or(T1.x, e.y);
+        } else {
+            lft = from_left_lane(T1.w);
+            rgt = from_right_lane(T1.x);
         }
         // step s+1 reads step s's guarded output: always finite
-        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true);
+        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v);
         if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb);
         if constexpr (WH) {
             bstore4<17>(K.rout, K.voff, o, (uint32_t)(p - 1 + A.gz) * K.pbytes);
@@ -735,6 +762,8 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         K.rout = __builtin_amdgcn_make_buffer_rsrc((void *)A.out, (short)0, nbytes, 0x00020000);
     }
     K.qwrap = (uint32_t)A.Lzg * K.qplane;  // < 2^32 quads (create_phi4)
+    K.m2v = f32x2{A.m2, A.m2};
+    asm volatile("" : "+v"(K.m2v));  // opaque: kept in VGPRs, not rematerialised from SGPRs per update
     // periodic: plane p+1 = nz is local plane 0 (tb_pidx); p never reaches it otherwise
     K.swrap_at = A.periodic ? A.nz - 2 : INT_MIN;  // slabs: p < 0 in ghost zones, never INT_MIN
     const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
