@@ -270,6 +270,9 @@ int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps);
  * generator it falls back to from the first exceptional call. */
 int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
                     unsigned int *w2, unsigned long long *seeds, double *xi, int generator);
+/* y[i] = f(x[i]) on the device with the serial order's float transcendentals
+ * (glibc's algorithms, csrc/sq_glibcf.h): fn 0 logf, 1 cosf, 2 tanhf. */
+int sq_selftest_libm(int device, int fn, const float *x, float *y, long long n);
 
 #ifdef __cplusplus
 }

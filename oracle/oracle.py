@@ -77,6 +77,7 @@ def lib():
         L.orc_serial_launch.argtypes = [ctypes.POINTER(SerialDev)]
         L.orc_ref_noise_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _D, _U32, _U32,
                                            ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_libm_f32.argtypes = [ctypes.c_int, _F, _F, ctypes.c_longlong]
         L.orc_phi4_step.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_uint64, ctypes.c_int]
         L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_uint64]
@@ -123,6 +124,14 @@ def qm1d_frame(N, a, dtau, pot, C, loops, seed, tick, runs, f, x, xx0, omega, lr
     lib().orc_qm1d_frame(ctypes.byref(s))
     return {"f": nf, "x": nx, "xx0": nxx0, "omega": s.nomega, "lrgEl": s.lrgEl, "lrgVl": s.lrgVl,
             "stable": s.stable, "steps_done": s.steps_done}
+
+
+def libm_f32(fn, x):
+    """The host libm's logf (fn 0), cosf (1) or tanhf (2) of a float32 array."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty_like(x)
+    lib().orc_libm_f32(fn, x.ctypes.data_as(_F), y.ctypes.data_as(_F), x.size)
+    return y
 
 
 def ref_noise_stream(seed, N, loops):

@@ -100,6 +100,13 @@ static double ref_random_words(uint64_t *seed, int gid, uint32_t *w1, uint32_t *
 
 double orc_ref_random(uint64_t *seed, int gid) { return ref_random_words(seed, gid, 0, 0); }
 
+void orc_libm_f32(int fn, const float *x, float *y, long long n)
+{
+#pragma omp parallel for schedule(static)
+    for (long long i = 0; i < n; ++i)
+        y[i] = fn == 0 ? logf(x[i]) : fn == 1 ? cosf(x[i]) : tanhf(x[i]);
+}
+
 /* The draws of one full launch in call order: rounds 0..loops-1, items
  * 0..N in id order, k = r*(N+1) + g.  seeds[k] is the
  * shared seed after call k, so a launch that breaks after call k leaves the

@@ -49,6 +49,11 @@ double orc_ref_random(uint64_t *seed, int gid);
 void orc_ref_noise_stream(uint64_t seed, int N, int loops, double *xi, uint32_t *w1, uint32_t *w2,
                           uint64_t *seeds);
 
+/* The host libm's float logf / cosf / tanhf (glibc: what the reference's
+ * random() and clas() evaluate, tau_kernel.cl:222,276-277), element-wise:
+ * fn 0 logf, 1 cosf, 2 tanhf.  The device restatement is checked against it. */
+void orc_libm_f32(int fn, const float *x, float *y, long long n);
+
 /* ---------------- physics helpers (tau_kernel.cl:184-267) ---------------- */
 double orc_xcl(double t, double w, int pot);
 double orc_ddpot(double x, int pot);

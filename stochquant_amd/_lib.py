@@ -145,6 +145,7 @@ SIGNATURES = {
     "sq_selftest_philox": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
                                           ctypes.POINTER(ctypes.c_uint)]),
     "sq_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, _D]),
+    "sq_selftest_libm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _F, _F, ctypes.c_longlong]),
 }
 
 _lib = None

@@ -2045,6 +2045,22 @@ int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int
     return SQ_OK;
 }
 
+int sq_selftest_libm(int device, int fn, const float *x, float *y, long long n) {
+    if (!x || !y || n < 0 || fn < 0 || fn > 2) return fail(SQ_E_ARG, "bad argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    if (n == 0) return SQ_OK;
+    DeviceGuard g(device);
+    float *d = nullptr;
+    SQ_HIP(hipMalloc(&d, 2 * (size_t)n * sizeof(float)));
+    hipError_t e = hipMemcpy(d, x, (size_t)n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = sq::selftest_libm_launch(fn, d, d + n, n, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(y, d + n, (size_t)n * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
 int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
                     unsigned int *w2, unsigned long long *seeds, double *xi, int generator) {
     if (!w1 || !w2 || !seeds || !xi || N < 1 || loops < 1) return fail(SQ_E_ARG, "bad argument");

@@ -21,6 +21,7 @@
 #include <cstdlib>
 
 #include "sq_dpp.h"
+#include "sq_glibcf.h"
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -36,7 +37,7 @@ constexpr int kMaxThreads = 1024;
 __device__ __forceinline__ double xcl(double t, double w, int pot) {  // clas(), :184-189,215-226
     if (pot == 3) {
         const double s = 2.0;  // (double)sqrtf((float)(2.*V0/m)) == 2 exactly
-        return kEta * (double)tanhf((float)(s * (t - w) / kEta));
+        return kEta * (double)sq_glibc_tanhf((float)(s * (t - w) / kEta));  // glibc's tanhf, bit for bit
     }
     return 0.;
 }

@@ -12,10 +12,10 @@
 //                    is a parallel prefix of affine maps (grid-wide) plus an
 //                    exact one-block fix-up from the first exception (below).
 //   gs_xi_kernel     grid-wide: xi = cos(2*3.1415*v2) * sqrt(-2 log v1) with
-//                    the reference's float casts (correctly rounded float
-//                    log/cos via fp64; glibc's logf/cosf round differently in
-//                    ~1% of arguments, so xi is within 1 ulp of the oracle's,
-//                    and bit-exact when the stream is injected).
+//                    the reference's float casts and glibc's own logf / cosf
+//                    algorithms (sq_glibcf.h, bit-identical to the host libm
+//                    the oracle and the reference use over every argument
+//                    random() can pass), so xi is the oracle's bit for bit.
 //   gs_omega_kernel  one wave: omega of every step (item N's scalar recurrence).
 //   gs_xcl_kernel    grid-wide, potID 3: x_cl and ddPot(x_cl) of every (step,
 //                    site), so the serial kernels below do no transcendentals.
@@ -40,6 +40,7 @@
 #include <cstdlib>
 
 #include "sq_dpp.h"
+#include "sq_glibcf.h"
 #include "sq_internal.h"
 
 namespace sq {
@@ -54,7 +55,7 @@ constexpr double kMax = 1000.;
 __device__ __forceinline__ double xcl(double t, double w, int pot) {  // clas(), :184-189,215-226
     if (pot == 3) {
         const double s = 2.0;  // (double)sqrtf((float)(2.*V0/m)) == 2 exactly
-        return kEta * (double)tanhf((float)(s * (t - w) / kEta));
+        return kEta * (double)sq_glibc_tanhf((float)(s * (t - w) / kEta));  // glibc's tanhf, bit for bit
     }
     return 0.;
 }
@@ -294,8 +295,8 @@ __global__ __launch_bounds__(256) void gs_xi_kernel(const uint32_t *w1, const ui
          k += (long long)gridDim.x * blockDim.x) {
         const double v1 = (double)w1[k] / two32;
         const double v2 = (double)w2[k] / two32;
-        const float lg = (float)log((double)(float)v1);
-        const float cs = (float)cos((double)(float)(2. * 3.1415 * v2));
+        const float lg = sq_glibc_logf((float)v1);
+        const float cs = sq_glibc_cosf((float)(2. * 3.1415 * v2));
         const float sq = sqrtf((float)(-2. * (double)lg));
         xi[k] = (double)cs * (double)sq;
     }

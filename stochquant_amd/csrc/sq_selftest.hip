@@ -3,6 +3,9 @@
 // RNG parity test), a DPP lane-rotation probe (the x-neighbour exchange of the
 // phi^4 kernel relies on wave_ror/wave_rol semantics), and a float4 streaming
 // copy that measures the attainable HBM rate on the box.
+#include <algorithm>
+
+#include "sq_glibcf.h"
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -28,6 +31,14 @@ __global__ void dpp_kernel(float *out) {
     const int v = lane;
     out[lane] = (float)__builtin_amdgcn_update_dpp(0, v, 0x13C, 0xF, 0xF, false);       // wave_ror:1
     out[64 + lane] = (float)__builtin_amdgcn_update_dpp(0, v, 0x134, 0xF, 0xF, false);  // wave_rol:1
+}
+
+// glibc's logf / cosf / tanhf as the serial-order QM1D kernels evaluate them
+// (sq_glibcf.h), for the bitwise test against the host libm.
+__global__ __launch_bounds__(256) void libm_kernel(int fn, const float *x, float *y, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        y[i] = fn == 0 ? sq_glibc_logf(x[i]) : fn == 1 ? sq_glibc_cosf(x[i]) : sq_glibc_tanhf(x[i]);
 }
 
 __global__ void philox_kernel(const uint32_t *ck, uint32_t *out) {
@@ -75,6 +86,12 @@ hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long
 
 hipError_t selftest_dpp_launch(float *out, hipStream_t s) {
     hipLaunchKernelGGL(dpp_kernel, dim3(1), dim3(64), 0, s, out);
+    return hipGetLastError();
+}
+
+hipError_t selftest_libm_launch(int fn, const float *x, float *y, long long n, hipStream_t s) {
+    const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 16384);
+    hipLaunchKernelGGL(libm_kernel, dim3(grid), dim3(256), 0, s, fn, x, y, n);
     return hipGetLastError();
 }
 

@@ -2,11 +2,12 @@
 reference's recorded outputs (tests/golden/reference_outputs.json).
 
 By default (N <= 4096) tauhost.o runs the reference's own serial order with
-its LCG seeded from the same rand() draw, so its trajectory reproduces the
-reference's to the 1-ulp budget of the float transcendentals; the formats,
-initial state (same unseeded glibc rand() draws, tauhost.c:84-102), first
-printed frame (xavg = 0 -> all -inf), Δτ controller sequence, omega for potID
-0 and trailer lines are bit-exact.  SQ_ORDER=jacobi (and N > 4096) runs the
+its LCG seeded from the same rand() draw and glibc's float log/cos/tanh
+algorithms on the device (csrc/sq_glibcf.h), so its stdout and end file are
+the serial oracle's byte for byte and the recorded reference values bit for
+bit: formats, initial state (same unseeded glibc rand() draws,
+tauhost.c:84-102), first printed frame (xavg = 0 -> all -inf), trajectory, Δτ
+controller sequence, omega and trailer lines.  SQ_ORDER=jacobi (and N > 4096) runs the
 Jacobi / Philox frame, checked statistically against its own exact law.
 """
 import re
@@ -124,10 +125,9 @@ def _hexrows(text, n):
 
 def test_serial_order_reproduces_appendix_c(gpu, oracle_mod, tmp_path):
     """Default order (no SQ_ORDER): the reference's serial order with its LCG
-    seeded from the same rand() draw.  The recorded end file (SURVEY.md
-    Appendix C) and the serial oracle's whole end file agree to the 1-ulp xi
-    budget (float log/cos rounding, tests/test_gpu_qm1d_serial.py); stdout,
-    omega, N, deltaTau exact."""
+    seeded from the same rand() draw and glibc's float log/cos on the device:
+    the recorded end-file line, the serial oracle's
+    whole end file, stdout, omega, N and deltaTau, all bit for bit."""
     g = golden("reference_outputs.json")["appendix_c_end_file"]
     out, end = _run(tmp_path, g["argv"])
     assert out.split("\n")[0] == g["stdout_first_line"]
@@ -135,15 +135,30 @@ def test_serial_order_reproduces_appendix_c(gpu, oracle_mod, tmp_path):
     assert el[4:7] == g["trailer"]
     got = _hexrows(end, 4)
     first = np.array([float.fromhex(t.strip()) for t in g["first_line"].split("|")])
-    assert np.allclose(got[0], first, rtol=1e-6, atol=1e-12)
+    assert np.array_equal(got[0], first), (got[0], first)
     ref_dir = tmp_path / "orc"
     ref_dir.mkdir()
     a = ["end" if v == "END" else v for v in g["argv"]]
     r = oracle_mod.tauhost(a, cwd=str(ref_dir))
     assert r.returncode == 0
     ref = _hexrows((ref_dir / "end").read_text(), 4)
-    assert np.allclose(got, ref, rtol=1e-6, atol=1e-12)
-    print("bit-exact sites:", int(np.sum(got == ref)), "of", got.size)
+    assert np.array_equal(got, ref), (got, ref)
+    assert end == (ref_dir / "end").read_text()
+
+
+@pytest.mark.parametrize("case", ["appendix_c_end_file", "double_well_all_unstable", "double_well_stable"])
+def test_reference_runs_byte_identical_to_oracle(gpu, oracle_mod, tmp_path, case):
+    """The recorded reference runs (potID 0 and the double-well presets, potID
+    3): tauhost.o's stdout and end file equal the serial oracle's byte for byte."""
+    g = golden("reference_outputs.json")[case]
+    out, end = _run(tmp_path, g["argv"])
+    ref_dir = tmp_path / "orc"
+    ref_dir.mkdir()
+    a = ["end" if v == "END" else v for v in g["argv"]]
+    r = oracle_mod.tauhost(a, cwd=str(ref_dir))
+    assert r.returncode == 0
+    assert out == r.stdout.decode()
+    assert end == (ref_dir / "end").read_text()
 
 
 def test_serial_order_all_unstable_preset(gpu, tmp_path):
