@@ -273,6 +273,11 @@ int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsig
 /* y[i] = f(x[i]) on the device with the serial order's float transcendentals
  * (glibc's algorithms, csrc/sq_glibcf.h): fn 0 logf, 1 cosf, 2 tanhf. */
 int sq_selftest_libm(int device, int fn, const float *x, float *y, long long n);
+/* The device's Box-Muller factors for every 23-bit argument m (4 x 2^23 floats,
+ * csrc/sq_rng.h): out[m] = sqrt(-2 ln u), out[2^23 + m] = sqrt(-log2 u),
+ * out[2*2^23 + m] = cos(t), out[3*2^23 + m] = sin(t), u = 2 - [1.m], t = [1.m]
+ * revolutions.  A device normal is one fp32 product of two entries. */
+int sq_selftest_bm_tables(int device, float *out);
 
 #ifdef __cplusplus
 }

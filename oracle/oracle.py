@@ -78,6 +78,7 @@ def lib():
         L.orc_ref_noise_stream.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _D, _U32, _U32,
                                            ctypes.POINTER(ctypes.c_uint64)]
         L.orc_libm_f32.argtypes = [ctypes.c_int, _F, _F, ctypes.c_longlong]
+        L.orc_set_bm_tables.argtypes = [_F]
         L.orc_phi4_step.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_uint64, ctypes.c_int]
         L.orc_phi4_step_slab.argtypes = [ctypes.POINTER(Phi4), _F, _F, ctypes.c_int, ctypes.c_uint64,
                                          ctypes.c_uint64]
@@ -124,6 +125,31 @@ def qm1d_frame(N, a, dtau, pot, C, loops, seed, tick, runs, f, x, xx0, omega, lr
     lib().orc_qm1d_frame(ctypes.byref(s))
     return {"f": nf, "x": nx, "xx0": nxx0, "omega": s.nomega, "lrgEl": s.lrgEl, "lrgVl": s.lrgVl,
             "stable": s.stable, "steps_done": s.steps_done}
+
+
+_BM_TABLES = None
+
+
+class device_transcendentals:
+    """Context manager: the oracle's normals use the device's Box-Muller
+    factors (sq_selftest_bm_tables, 4 x 2^23 float32), so its noise -- and with
+    it every noise-on result -- is the GPU's bit for bit."""
+
+    def __init__(self, tables):
+        self.tables = np.ascontiguousarray(tables, dtype=np.float32)
+        assert self.tables.size == 4 << 23
+
+    def __enter__(self):
+        global _BM_TABLES
+        _BM_TABLES = self.tables  # keep the buffer alive while the C side points at it
+        lib().orc_set_bm_tables(self.tables.ctypes.data_as(_F))
+        return self
+
+    def __exit__(self, *exc):
+        global _BM_TABLES
+        lib().orc_set_bm_tables(None)
+        _BM_TABLES = None
+        return False
 
 
 def libm_f32(fn, x):

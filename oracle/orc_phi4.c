@@ -14,10 +14,9 @@
  *   φ'   = fma(σ, ξ, fma(Δτ, drift, φ)),     σ = C·sqrt(2Δτ) (C = 1 physical)
  *   φ'   = NaN ? max : clamp(φ', -max, max)
  *
- * The evaluation order is the product's (fp32, explicit fma); the only
- * GPU-vs-oracle difference is ξ, whose hardware transcendentals are compared
- * with the double-evaluated value here under the tolerance stated in
- * tests/test_gpu_parity.py.  Site index s = (z·Ly + y)·Lx + x (global),
+ * The evaluation order is the product's (fp32, explicit fma).  ξ is the
+ * double-evaluated normal by default, or (orc_set_bm_tables) the device's own
+ * Box-Muller factors, with which the result is the GPU's bit for bit.  Site index s = (z·Ly + y)·Lx + x (global),
  * noise quad s>>2, component s&3, stream 0.
  */
 #include <math.h>
@@ -30,6 +29,9 @@
 #endif
 
 float orc_phi4_sigma(float h, double C) { return (float)(sqrt(2.0 * (double)h) * C); }
+/* sigma * sqrt(2 ln 2): the amplitude of the kernels' box_muller_q pairs
+ * (sq_api.cpp phi4_base_args, kSqrt2Ln2 = 1.1774100225154747). */
+float orc_phi4_sigq(float h, double C) { return (float)(sqrt(2.0 * (double)h) * C * 1.1774100225154747); }
 float orc_phi4_lam6(float lam) { return (float)((double)lam / 6.0); }
 
 /* Order-preserving float -> uint32 map (larger float, larger code). */
@@ -61,7 +63,9 @@ static void phi4_plane(const orc_phi4 *p, const float *cz, const float *czmp, co
 {
     const int Lx = p->Lx, Ly = p->Ly;
     const float h = p->h, m2 = p->m2, lam6 = orc_phi4_lam6(p->lam);
-    const float sig = orc_phi4_sigma(h, p->C), mx = p->clampv;
+    /* device-transcendental mode: the kernels' exact noise (q pairs, sigq) */
+    const int dev = orc_bm_tables_on();
+    const float sig = dev ? orc_phi4_sigq(h, p->C) : orc_phi4_sigma(h, p->C), mx = p->clampv;
     for (int y = 0; y < Ly; ++y) {
         const int ym = (y + Ly - 1) % Ly, yp = (y + 1) % Ly;
         const float *c = cz + (size_t)y * Lx;
@@ -73,7 +77,10 @@ static void phi4_plane(const orc_phi4 *p, const float *cz, const float *czmp, co
         const uint64_t row0 = (zg * (uint64_t)Ly + (uint64_t)y) * (uint64_t)Lx;
         for (int x0 = 0; x0 < Lx; x0 += 4) {
             float xi[4];
-            orc_normals4(p->seed, 0, (row0 + (uint64_t)x0) >> 2, step, xi);
+            if (dev)
+                orc_normals4_q(p->seed, 0, (row0 + (uint64_t)x0) >> 2, step, xi);
+            else
+                orc_normals4(p->seed, 0, (row0 + (uint64_t)x0) >> 2, step, xi);
             for (int k = 0; k < 4; ++k) {
                 const int x = x0 + k;
                 const int xm = (x + Lx - 1) % Lx, xp = (x + 1) % Lx;

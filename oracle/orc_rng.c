@@ -43,14 +43,53 @@ void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t ou
  *   u = 1 - (w0 & 0x7FFFFF) * 2^-23   in (0,1], exact in fp32
  *   t = (w1 & 0x7FFFFF) * 2^-23       in [0,1) revolutions, exact in fp32
  *   n_cos = sqrt(-2 ln u) cos(2 pi t),  n_sin = sqrt(-2 ln u) sin(2 pi t) */
+/* Device-transcendental mode (orc_set_bm_tables): the MI355X's Box-Muller
+ * factors for every 23-bit argument, as sq_selftest_bm_tables returns them
+ * (radius sqrt(-2 ln u), radius_q sqrt(-log2 u), cos, sin; 2^23 each).  A
+ * device normal is then one fp32 product of two entries, so the oracle gives
+ * the GPU's bits; the entries themselves are checked against the
+ * double-evaluated values (tests/test_gpu_selftest.py). */
+#define BM_N ((size_t)1 << 23)
+static const float *g_bm = NULL;
+
+void orc_set_bm_tables(const float *tab) { g_bm = tab; }
+int orc_bm_tables_on(void) { return g_bm != NULL; }
+
 static void bm_pair(uint32_t w0, uint32_t w1, float *nc, float *ns)
 {
+    if (g_bm) {
+        const float r = g_bm[w0 & 0x7FFFFFu];
+        *nc = r * g_bm[2 * BM_N + (w1 & 0x7FFFFFu)];
+        *ns = r * g_bm[3 * BM_N + (w1 & 0x7FFFFFu)];
+        return;
+    }
     const double u = 1.0 - (double)(w0 & 0x7FFFFFu) * 0x1p-23;
     const double t = (double)(w1 & 0x7FFFFFu) * 0x1p-23;
     const double r = sqrt(-2.0 * log(u));
     const double ang = 2.0 * M_PI * t;
     *nc = (float)(r * cos(ang));
     *ns = (float)(r * sin(ang));
+}
+
+/* The phi^4 kernels' field noise in device-transcendental mode: the pairs
+ * without the sqrt(2 ln 2) factor (box_muller_q), which sigq carries. */
+static void bm_pair_q(uint32_t w0, uint32_t w1, float *nc, float *ns)
+{
+    const float r = g_bm[BM_N + (w0 & 0x7FFFFFu)];
+    *nc = r * g_bm[2 * BM_N + (w1 & 0x7FFFFFu)];
+    *ns = r * g_bm[3 * BM_N + (w1 & 0x7FFFFFu)];
+}
+
+void orc_normals4_q(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4])
+{
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {(uint32_t)quad,
+                       ((uint32_t)(quad >> 32) & 0x00FFFFFFu) | (stream << 24),
+                       (uint32_t)step, (uint32_t)(step >> 32)};
+    uint32_t o[4];
+    orc_philox4x32_10(ctr, key, o);
+    bm_pair_q(o[0], o[1], &out[0], &out[1]);
+    bm_pair_q(o[2], o[3], &out[2], &out[3]);
 }
 
 void orc_normals4(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4])

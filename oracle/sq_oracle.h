@@ -42,6 +42,13 @@ extern "C" {
 void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Four standard normals for (seed, stream, quad, step); layout in DESIGN.md §RNG. */
 void orc_normals4(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4]);
+/* Device-transcendental mode: tab = the 4 x 2^23 Box-Muller factors of
+ * sq_selftest_bm_tables (NULL: back to the double-evaluated normals).  While
+ * set, orc_normals4 is the device's normals4 bit for bit and the phi^4 steps
+ * draw the kernels' box_muller_q pairs scaled by sigq (orc_phi4_sigq). */
+void orc_set_bm_tables(const float *tab);
+int orc_bm_tables_on(void);
+void orc_normals4_q(uint64_t seed, uint32_t stream, uint64_t quad, uint64_t step, float out[4]);
 /* The reference's shared-seed LCG + Box-Muller, tau_kernel.cl:269-284. */
 double orc_ref_random(uint64_t *seed, int gid);
 /* All draws of one full launch in call order (k = round*(N+1) + item), the

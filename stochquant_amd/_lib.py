@@ -146,6 +146,7 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_uint)]),
     "sq_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, _D]),
     "sq_selftest_libm": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _F, _F, ctypes.c_longlong]),
+    "sq_selftest_bm_tables": (ctypes.c_int, [ctypes.c_int, _F]),
 }
 
 _lib = None

@@ -2061,6 +2061,21 @@ int sq_selftest_libm(int device, int fn, const float *x, float *y, long long n) 
     return SQ_OK;
 }
 
+int sq_selftest_bm_tables(int device, float *out) {
+    if (!out) return fail(SQ_E_ARG, "null argument");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    const size_t bytes = 4 * ((size_t)1 << 23) * sizeof(float);
+    float *d = nullptr;
+    SQ_HIP(hipMalloc(&d, bytes));
+    hipError_t e = sq::selftest_bm_tables_launch(d, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(out, d, bytes, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
 int sq_selftest_lcg(int device, unsigned long long seed, int N, int loops, unsigned int *w1,
                     unsigned int *w2, unsigned long long *seeds, double *xi, int generator) {
     if (!w1 || !w2 || !seeds || !xi || N < 1 || loops < 1) return fail(SQ_E_ARG, "bad argument");

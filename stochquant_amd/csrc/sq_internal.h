@@ -165,6 +165,7 @@ hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long
 hipError_t selftest_dpp_launch(float *out, hipStream_t s);
 hipError_t selftest_philox_launch(const uint32_t *ck, uint32_t *out, hipStream_t s);
 hipError_t selftest_libm_launch(int fn, const float *x, float *y, long long n, hipStream_t s);
+hipError_t selftest_bm_tables_launch(float *t, hipStream_t s);
 hipError_t copy_launch(const float4 *in, float4 *out, size_t n4, bool nt, hipStream_t s);
 
 }  // namespace sq

@@ -55,15 +55,26 @@ __device__ __forceinline__ u32x4 philox_counter(uint64_t quad, uint32_t stream, 
                  step_hi};
 }
 
+// The four factors of a pair, each a function of 23 bits of one word (so
+// sq_selftest_bm_tables can tabulate them, and the oracle reproduce a
+// device normal bit for bit as one fp32 product of two table entries):
+//   u = 2 - [1.m0] in (0,1] (exact, Sterbenz), t = [1.m1] in [1,2) revolutions
+//   (one v_and_or_b32 each; cos/sin have period 1 revolution, so t needs no "- 1").
+__device__ __forceinline__ float bm_u(uint32_t w0) { return 2.0f - __uint_as_float(0x3F800000u | (w0 & 0x007FFFFFu)); }
+__device__ __forceinline__ float bm_t(uint32_t w1) { return __uint_as_float(0x3F800000u | (w1 & 0x007FFFFFu)); }
+__device__ __forceinline__ float bm_radius(uint32_t w0) {  // sqrt(-2 ln u) = sqrt(-2 ln 2 * log2 u)
+    return __builtin_amdgcn_sqrtf(__builtin_amdgcn_logf(bm_u(w0)) * -1.38629436111989061f);
+}
+__device__ __forceinline__ float bm_radius_q(uint32_t w0) {  // sqrt(-log2 u)
+    return __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(bm_u(w0)));
+}
+__device__ __forceinline__ float bm_cos(uint32_t w1) { return __builtin_amdgcn_cosf(bm_t(w1)); }
+__device__ __forceinline__ float bm_sin(uint32_t w1) { return __builtin_amdgcn_sinf(bm_t(w1)); }
+
 __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float &nc, float &ns) {
-    // 23 mantissa bits of each word placed in [1,2) by one v_and_or_b32:
-    //   u = 2 - [1.m0] in (0,1] (exact, Sterbenz), t = [1.m1] in [1,2) revolutions;
-    //   cos/sin have period 1 revolution, so t needs no "- 1".
-    const float u = 2.0f - __uint_as_float(0x3F800000u | (w0 & 0x007FFFFFu));
-    const float t = __uint_as_float(0x3F800000u | (w1 & 0x007FFFFFu));
-    const float r = __builtin_amdgcn_sqrtf(__builtin_amdgcn_logf(u) * -1.38629436111989061f);
-    nc = r * __builtin_amdgcn_cosf(t);
-    ns = r * __builtin_amdgcn_sinf(t);
+    const float r = bm_radius(w0);
+    nc = r * bm_cos(w1);
+    ns = r * bm_sin(w1);
 }
 
 // Box-Muller without the sqrt(2 ln 2) factor: r' = sqrt(-log2 u), so the pair
@@ -71,11 +82,9 @@ __device__ __forceinline__ void box_muller(uint32_t w0, uint32_t w1, float &nc, 
 // factor into their noise amplitude (Phi4StepArgs::sigq = sigma sqrt(2 ln 2)),
 // which saves one multiply per pair; the sign flip is a free source modifier.
 __device__ __forceinline__ void box_muller_q(uint32_t w0, uint32_t w1, float &nc, float &ns) {
-    const float u = 2.0f - __uint_as_float(0x3F800000u | (w0 & 0x007FFFFFu));
-    const float t = __uint_as_float(0x3F800000u | (w1 & 0x007FFFFFu));
-    const float r = __builtin_amdgcn_sqrtf(-__builtin_amdgcn_logf(u));
-    nc = r * __builtin_amdgcn_cosf(t);
-    ns = r * __builtin_amdgcn_sinf(t);
+    const float r = bm_radius_q(w0);
+    nc = r * bm_cos(w1);
+    ns = r * bm_sin(w1);
 }
 
 struct f32x4n {

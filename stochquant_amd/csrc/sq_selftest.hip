@@ -41,6 +41,17 @@ __global__ __launch_bounds__(256) void libm_kernel(int fn, const float *x, float
         y[i] = fn == 0 ? sq_glibc_logf(x[i]) : fn == 1 ? sq_glibc_cosf(x[i]) : sq_glibc_tanhf(x[i]);
 }
 
+// The Box-Muller factors of every 23-bit argument (sq_rng.h): radius
+// sqrt(-2 ln u), radius_q sqrt(-log2 u), cos and sin of t revolutions.
+__global__ __launch_bounds__(256) void bm_tables_kernel(float *rad, float *radq, float *cs, float *sn) {
+    const uint32_t m = blockIdx.x * 256u + threadIdx.x;
+    if (m >= (1u << 23)) return;
+    rad[m] = bm_radius(m);
+    radq[m] = bm_radius_q(m);
+    cs[m] = bm_cos(m);
+    sn[m] = bm_sin(m);
+}
+
 __global__ void philox_kernel(const uint32_t *ck, uint32_t *out) {
     const u32x4 o = philox4x32_10(u32x4{ck[0], ck[1], ck[2], ck[3]}, ck[4], ck[5]);
     out[0] = o.x;
@@ -92,6 +103,12 @@ hipError_t selftest_dpp_launch(float *out, hipStream_t s) {
 hipError_t selftest_libm_launch(int fn, const float *x, float *y, long long n, hipStream_t s) {
     const unsigned grid = (unsigned)std::min<long long>((n + 255) / 256, 16384);
     hipLaunchKernelGGL(libm_kernel, dim3(grid), dim3(256), 0, s, fn, x, y, n);
+    return hipGetLastError();
+}
+
+hipError_t selftest_bm_tables_launch(float *t, hipStream_t s) {
+    const size_t n = (size_t)1 << 23;
+    hipLaunchKernelGGL(bm_tables_kernel, dim3((unsigned)(n / 256)), dim3(256), 0, s, t, t + n, t + 2 * n, t + 3 * n);
     return hipGetLastError();
 }
 

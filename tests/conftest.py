@@ -58,6 +58,25 @@ def sqlib():
 
 
 @pytest.fixture(scope="session")
+def bm_tables(gpu, sqlib):
+    """The device's Box-Muller factors for every 23-bit argument (4 x 2^23
+    float32, sq_selftest_bm_tables): with them the oracle's noise is the GPU's
+    bit for bit (oracle.device_transcendentals)."""
+    import ctypes
+    import numpy as np
+    t = np.empty(4 << 23, np.float32)
+    assert sqlib.sq_selftest_bm_tables(0, t.ctypes.data_as(ctypes.POINTER(ctypes.c_float))) == 0
+    return t
+
+
+@pytest.fixture
+def dev_oracle(oracle_mod, bm_tables):
+    """The oracle in device-transcendental mode for the duration of one test."""
+    with oracle_mod.device_transcendentals(bm_tables):
+        yield oracle_mod
+
+
+@pytest.fixture(scope="session")
 def gpu(sqlib):
     """Skip-free GPU gate: gpu-marked tests must run on a box with a device and fail loudly otherwise."""
     from stochquant_amd import _lib

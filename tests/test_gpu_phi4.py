@@ -3,11 +3,16 @@
 Parity contract (fp32):
   * C = 0 (noise off): the GPU step is BIT-IDENTICAL to the oracle -- same
     fp32 operations in the same order (explicit fma, -ffp-contract=off).
-  * C = 1: the only difference is the hardware transcendentals of the noise;
-    one step differs by at most  sigma*(NORMAL_ATOL + NORMAL_RTOL*|xi|) plus one
-    rounding of phi', i.e.  |d| <= STEP_ATOL + STEP_RTOL*|phi'|  per step, and
-    the update is a contraction for these parameters (row sum of the Jacobian
-    1 - h*V'' < 1), so k steps stay within k times that bound.
+  * C = 1: the only difference from the mathematical oracle is the hardware
+    transcendentals of the noise; one step differs by at most
+    sigma*(NORMAL_ATOL + NORMAL_RTOL*|xi|) plus one rounding of phi', i.e.
+    |d| <= STEP_ATOL + STEP_RTOL*|phi'|  per step, and the update is a
+    contraction for these parameters (row sum of the Jacobian 1 - h*V'' < 1),
+    so k steps stay within k times that bound.  With the device's own
+    Box-Muller factors (the `dev_oracle` fixture: v_log/v_sqrt/v_cos/v_sin of
+    every 23-bit argument, tabulated on the GPU and checked for accuracy in
+    test_gpu_selftest.py) the oracle draws the GPU's normals and every C = 1
+    result is BIT-IDENTICAL as well (`*_bitwise_device_transcendentals`).
   * Slab decomposition (loopback slabs, RCCL self-exchange) is bit-identical
     to the monolithic run with the noise on.
 """
@@ -72,6 +77,17 @@ def test_noisy_step_within_tolerance(gpu, oracle_mod, shape):
     assert np.all(err <= bound)
 
 
+@pytest.mark.parametrize("shape", SHAPES)
+def test_noisy_step_bitwise_device_transcendentals(gpu, dev_oracle, shape):
+    phi0 = _init(dev_oracle, shape)
+    with _lat(shape) as L:
+        L.upload(phi0)
+        L.step(4)
+        got = L.download()
+    ref = _oracle_run(dev_oracle, shape, phi0, 4)
+    assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+
+
 @pytest.mark.parametrize("shape,nslabs", [((16, 16, 16), 2), ((32, 8, 13), 3), ((256, 4, 33), 5),
                                           ((64, 16, 8), 8), ((512, 4, 6), 2)])
 def test_loopback_decomposition_bitwise(gpu, oracle_mod, shape, nslabs):
@@ -102,8 +118,9 @@ def test_rccl_self_exchange_bitwise(gpu, oracle_mod):
     assert np.array_equal(mono, got)
 
 
-def test_full_size_256_one_step(gpu, oracle_mod):
-    """BASELINE config C2 (256^3 fp32): one step vs the oracle, and the
+def test_full_size_256_one_step(gpu, oracle_mod, bm_tables):
+    """BASELINE config C2 (256^3 fp32): one step vs the oracle (within the
+    tolerance of the mathematical normals, bitwise with the device's), and the
     decomposition invariance at full size."""
     shape = (256, 256, 256)
     phi0 = _init(oracle_mod, shape, amp=0.5)
@@ -114,6 +131,8 @@ def test_full_size_256_one_step(gpu, oracle_mod):
     ref = _oracle_run(oracle_mod, shape, phi0, 1, dtau=0.01, m2=1.0, lam=1.0)
     err = np.abs(got.astype(np.float64) - ref)
     assert np.all(err <= STEP_ATOL + STEP_RTOL * np.abs(ref))
+    with oracle_mod.device_transcendentals(bm_tables):
+        assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 1, dtau=0.01, m2=1.0, lam=1.0))
     with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, comm="loopback", nslabs=4) as L:
         L.upload(phi0)
         L.step(1)
@@ -154,13 +173,15 @@ def test_stable_frames_grow_dtau(gpu, oracle_mod):
         assert L.dtau == pytest.approx(d0 / 0.95)  # tauhost.c:523-528: after 11 stable frames
 
 
-def test_init_field_matches_oracle(gpu, oracle_mod):
+def test_init_field_matches_oracle(gpu, oracle_mod, bm_tables):
     shape = (64, 16, 8)
     with _lat(shape, seed=77) as L:
         L.init_field(0.9)
         got = L.download()
     ref = _init(oracle_mod, shape, amp=0.9, seed=77)
     assert np.all(np.abs(got - ref) <= 0.9 * (2e-6 + 2e-6 * np.abs(ref / 0.9)))
+    with oracle_mod.device_transcendentals(bm_tables):
+        assert np.array_equal(got, _init(oracle_mod, shape, amp=0.9, seed=77))
 
 
 def test_moments_and_correlator(gpu, oracle_mod):
@@ -253,9 +274,10 @@ def test_prefetch_variants_bitwise(gpu, oracle_mod, monkeypatch, shape, pf):
     assert np.array_equal(got, _oracle_run(oracle_mod, shape, phi0, 3, C=0.0))
 
 
-def _full_size_check(oracle_mod, shape, steps, **kw):
+def _full_size_check(oracle_mod, shape, steps, tables=None, **kw):
     """`steps` steps of the lattice context built with **kw, C = 0 (bitwise) and
-    C = 1 (per-step tolerance) vs the oracle, returning the C = 1 field."""
+    C = 1 vs the oracle -- bitwise with the device's Box-Muller factors
+    (`tables`), else within the per-step tolerance -- returning the C = 1 field."""
     from stochquant_amd import unique_id
     phi0 = _init(oracle_mod, shape, amp=0.5)
     out = None
@@ -267,6 +289,13 @@ def _full_size_check(oracle_mod, shape, steps, **kw):
             L.step(steps)
             got = L.download()
             kname = L.kernel_name
+        if C == 1.0 and tables is not None:
+            with oracle_mod.device_transcendentals(tables):
+                ref = _oracle_run(oracle_mod, shape, phi0, steps, C=C, dtau=0.01, m2=1.0, lam=1.0)
+            assert np.array_equal(got, ref), f"{kname} (C = 1): max diff {np.max(np.abs(got - ref))}"
+            out = got
+            del got, ref
+            continue
         ref = _oracle_run(oracle_mod, shape, phi0, steps, C=C, dtau=0.01, m2=1.0, lam=1.0)
         if C == 0.0:
             assert np.array_equal(got, ref), f"{kname}: max diff {np.max(np.abs(got - ref))}"
@@ -278,14 +307,15 @@ def _full_size_check(oracle_mod, shape, steps, **kw):
     return phi0, out
 
 
-def test_full_size_512(gpu, oracle_mod):
+def test_full_size_512(gpu, oracle_mod, bm_tables):
     """BASELINE config C3 (512^3 fp32, 2 x 512 MiB, the HBM-bound case): two
-    steps (one launch pair of whatever the library runs at 512^3) vs the oracle."""
-    _full_size_check(oracle_mod, (512, 512, 512), 2)
+    steps (one launch pair of whatever the library runs at 512^3) vs the
+    oracle, bitwise at C = 0 and (device Box-Muller factors) at C = 1."""
+    _full_size_check(oracle_mod, (512, 512, 512), 2, tables=bm_tables)
 
 
 @pytest.mark.parametrize("ghost", ["16", "auto"])
-def test_c5_slab_1024x1024x128_rccl(gpu, oracle_mod, monkeypatch, ghost):
+def test_c5_slab_1024x1024x128_rccl(gpu, oracle_mod, bm_tables, monkeypatch, ghost):
     """BASELINE config C5's per-GPU slab (1024^3 over 8 GPUs = 1024 x 1024 x 128
     planes per rank) through the RCCL slab path (self-exchange: the same
     deep-halo blocks, exchange and stream joins as a multi-rank run), G = 16
@@ -297,7 +327,7 @@ def test_c5_slab_1024x1024x128_rccl(gpu, oracle_mod, monkeypatch, ghost):
         monkeypatch.setenv("SQ_GHOST_AUTO", "1")
     else:
         monkeypatch.setenv("SQ_GHOST", ghost)
-    phi0, _ = _full_size_check(oracle_mod, shape, 1, comm="rccl")
+    phi0, _ = _full_size_check(oracle_mod, shape, 1, tables=bm_tables, comm="rccl")
     with _lat(shape, dtau=0.01, m2=1.0, lam=1.0) as L:
         L.upload(phi0)
         L.step(100)
@@ -310,14 +340,14 @@ def test_c5_slab_1024x1024x128_rccl(gpu, oracle_mod, monkeypatch, ghost):
         assert np.array_equal(L.download(), mono)
 
 
-def test_full_size_256_rccl_slab_fused_vs_oracle(gpu, oracle_mod, monkeypatch):
+def test_full_size_256_rccl_slab_fused_vs_oracle(gpu, oracle_mod, bm_tables, monkeypatch):
     """C2/C4's per-GPU slab through the RCCL slab path with the inner steps of
     each block fused in pairs (G = 4: core/rim step 0, a pair, the edges-first
-    last step): 4 steps vs the oracle -- bitwise at C = 0, within 4 steps'
-    tolerance at C = 1."""
+    last step): 4 steps vs the oracle -- bitwise at C = 0 and, with the
+    device's Box-Muller factors, at C = 1."""
     monkeypatch.setenv("SQ_GHOST", "4")
     monkeypatch.setenv("SQ_FUSE2", "1")
-    _full_size_check(oracle_mod, (256, 256, 256), 4, comm="rccl")
+    _full_size_check(oracle_mod, (256, 256, 256), 4, tables=bm_tables, comm="rccl")
 
 
 FUSE2_SHAPES = [(256, 8, 2), (256, 8, 5), (256, 16, 12), (256, 32, 33), (256, 64, 64), (256, 24, 17),
@@ -662,9 +692,10 @@ def test_stability_rule_rolls_back_diverging_unclamped_field(gpu, oracle_mod, mo
         assert L.step_counter == loops                      # a retried frame draws fresh noise
 
 
-def test_stability_rule_quiet_on_stable_frames(gpu, oracle_mod):
+def test_stability_rule_quiet_on_stable_frames(gpu, oracle_mod, bm_tables):
     """dtau = 0.01, noise on: the heuristic never fires, records within the
-    noise tolerance of the oracle's (hardware transcendentals in xi)."""
+    noise tolerance of the mathematical oracle's and identical to the
+    oracle's with the device's Box-Muller factors."""
     shape, loops = (256, 16, 16), 6
     phi0 = _init(oracle_mod, shape, amp=0.3)
     p = oracle_mod.phi4_params(shape, 0.01, 1.0, 1.0, 1234, C=1.0)
@@ -679,4 +710,13 @@ def test_stability_rule_quiet_on_stable_frames(gpu, oracle_mod):
         tol = loops * (STEP_ATOL + STEP_RTOL * 4.0)
         assert np.allclose(st["M"], M, atol=tol) and np.allclose(st["A"], A, atol=tol)
         assert np.allclose(st["D"], D, atol=tol)
-        assert np.allclose(L.download(), out, atol=tol)
+        got = L.download()
+        assert np.allclose(got, out, atol=tol)
+    # the device's Box-Muller factors: records, T, V and the field bit for bit
+    with oracle_mod.device_transcendentals(bm_tables):
+        out, M, D, A, fired, T1, V1 = oracle_mod.phi4_frame_stab(p, phi0, loops, 0, float(phi0.max()),
+                                                                float(np.abs(phi0).max()))
+    assert fired == -1
+    assert np.array_equal(st["M"], M) and np.array_equal(st["D"], D) and np.array_equal(st["A"], A)
+    assert st["T"] == T1 and st["V"] == V1
+    assert np.array_equal(got, out)

@@ -71,6 +71,24 @@ def test_frame_within_tolerance(gpu, oracle_mod, N, pot, C):
     assert abs(d["omega"] - r["omega"]) <= loops * 1e-5
 
 
+@pytest.mark.parametrize("N,pot,C", [(200, 0, 1.0), (1000, 0, 1.0), (200, 3, 1.0), (4096, 3, 1.0),
+                                     (8192, 0, 1.0), (65536, 3, 1.0)])
+def test_frame_bitwise_device_transcendentals(gpu, dev_oracle, N, pot, C):
+    """The same frames with the device's Box-Muller factors in the oracle
+    (x_cl's tanhf is glibc's on both sides): f, x, xx0, omega and the scan
+    bit for bit."""
+    a, h, loops = 0.1, 0.002, 40
+    f, x, xx0 = _state(N)
+    om = N * a / 2 + 0.013
+    stable, d, sc = _gpu_frame(N, a, h, pot, C, loops, 21, f, x, xx0, om, runs=3, lrgVl=1.0)
+    r = dev_oracle.qm1d_frame(N, a, h, pot, C, loops, 21, 0, 3, f, x, xx0, om, 0, 1.0)
+    assert r["stable"] == 1 and stable
+    for k in ("f", "x", "xx0"):
+        assert np.array_equal(d[k], r[k]), (k, np.max(np.abs(d[k] - r[k])))
+    assert d["omega"] == r["omega"]
+    assert sc["lrgEl"] == r["lrgEl"] and sc["lrgVl"] == r["lrgVl"]
+
+
 def test_unstable_frame_detected_and_rolled_back(gpu, oracle_mod):
     """The double-well preset with Δτ/Δt² = 5 (taumain.py:101-108 at dt=0.02)
     blows up in any ordering: both sides flag the frame, the state is kept."""

@@ -49,6 +49,25 @@ def test_normals_match_oracle(gpu, sqlib, oracle_mod, stream, quad0, step):
     assert np.all(err <= bound)
 
 
+def test_bm_tables_accuracy(gpu, bm_tables):
+    """The device's Box-Muller factors (the tables the oracle's
+    device-transcendental mode uses) against the double-evaluated functions:
+    v_log_f32 / v_sqrt_f32 / v_cos_f32 / v_sin_f32 of every 23-bit argument."""
+    n = 1 << 23
+    m = np.arange(n, dtype=np.float64)
+    u = 1.0 - m * 2.0 ** -23
+    t = m * 2.0 ** -23
+    rad, radq, cs, sn = (bm_tables[k * n:(k + 1) * n].astype(np.float64) for k in range(4))
+    r_ex = np.sqrt(-2.0 * np.log(u))
+    rq_ex = np.sqrt(-np.log2(u))
+    for got, ex in ((rad, r_ex), (radq, rq_ex)):
+        assert np.all(np.abs(got - ex) <= 1e-6 + 1e-6 * ex)
+    assert np.all(np.abs(cs - np.cos(2 * np.pi * t)) <= 2e-6)
+    assert np.all(np.abs(sn - np.sin(2 * np.pi * t)) <= 2e-6)
+    print("max |r - exact| rel", np.max(np.abs(rad - r_ex) / np.maximum(r_ex, 1e-30)),
+          "max |cos - exact|", np.max(np.abs(cs - np.cos(2 * np.pi * t))))
+
+
 def test_copy_bandwidth_runs(gpu, sqlib):
     g = ctypes.c_double()
     assert sqlib.sq_copy_bandwidth(0, 1 << 28, 10, ctypes.byref(g)) == 0
