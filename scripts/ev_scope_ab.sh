@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of the slab path's event fence scope (SQ_EV_SCOPE), RCCL
-# (The SQ_EV_SCOPE knob existed only for this A/B; it was removed after it: no gain.)
 # self-exchange at 256^3, plus the bitwise slab tests under the candidate.
+# (The SQ_EV_SCOPE knob existed only for this A/B; it was removed after it: no gain.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/ev_scope
 mkdir -p $O
