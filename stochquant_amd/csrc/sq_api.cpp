@@ -177,11 +177,18 @@ struct sq_ctx {
     bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
                             // (SQ_CORE_PAIRS pins; multi-rank runs time 1, 2, 4 on the real link)
     double *dacc = nullptr;
+    double *dpart = nullptr;       // moments: per-block partials (sq::kMomBlocks x 4)
+    double *dslice = nullptr;      // correlator: slice sums of the global lattice (Lz), allocated once
     unsigned int *dmax = nullptr;  // [0] max |phi| bits, [1] ordered max phi
     // stability heuristic of phi4 frames (tau_kernel.cl:135-143):
     // per-step device records of the current frame, kStabSlots words per step
     unsigned long long *st_md = nullptr;
     unsigned int *st_a = nullptr;
+    // phi^4 frames: st_md | st_a | flag in ONE device block (one memset, one
+    // read-back per frame) and its pinned host mirror
+    void *frame_rec = nullptr;
+    void *frame_host = nullptr;
+    size_t frame_bytes = 0;
     unsigned long long frame_step0 = 0;  // Philox step of the frame's first step
     bool stab_init = false;              // T, V set from the field at the first frame
     float stab_T = 0, stab_V = 0;        // carried across frames, never rolled back (as lrgEl / lrgVl)
@@ -944,14 +951,22 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         SQ_HIP(hipEventRecord(s.evE, s.sA));
     }
-    SQ_HIP(hipMalloc(&c->flag, sizeof(int)));
-    SQ_HIP(hipMemset(c->flag, 0, sizeof(int)));
-    SQ_HIP(hipMalloc(&c->dacc, 2 * sizeof(double)));
-    SQ_HIP(hipMalloc(&c->dmax, 2 * sizeof(unsigned int)));
-    if (p.loops >= 1) {
-        SQ_HIP(hipMalloc(&c->st_md, sizeof(unsigned long long) * sq::kStabSlots * (size_t)p.loops));
-        SQ_HIP(hipMalloc(&c->st_a, sizeof(unsigned int) * sq::kStabSlots * (size_t)p.loops));
+    {
+        const size_t nrec = (size_t)sq::kStabSlots * (size_t)std::max(p.loops, 0);
+        c->frame_bytes = nrec * (sizeof(unsigned long long) + sizeof(unsigned int)) + 2 * sizeof(int);
+        SQ_HIP(hipMalloc(&c->frame_rec, c->frame_bytes));
+        SQ_HIP(hipMemset(c->frame_rec, 0, c->frame_bytes));
+        SQ_HIP(hipHostMalloc(&c->frame_host, c->frame_bytes, hipHostMallocDefault));
+        char *b = static_cast<char *>(c->frame_rec);
+        if (nrec > 0) {
+            c->st_md = reinterpret_cast<unsigned long long *>(b);
+            c->st_a = reinterpret_cast<unsigned int *>(b + nrec * sizeof(unsigned long long));
+        }
+        c->flag = reinterpret_cast<int *>(b + nrec * (sizeof(unsigned long long) + sizeof(unsigned int)));
     }
+    SQ_HIP(hipMalloc(&c->dacc, 2 * sizeof(double)));
+    SQ_HIP(hipMalloc(&c->dpart, 4 * sizeof(double) * sq::kMomBlocks));
+    SQ_HIP(hipMalloc(&c->dmax, 2 * sizeof(unsigned int)));
     if (p.comm == SQ_COMM_RCCL) {
         ncclUniqueId id;
         static_assert(sizeof(id.internal) <= 128, "ncclUniqueId size");
@@ -1245,10 +1260,8 @@ int phi4_field_max(sq_ctx *c, float *mx_phi, float *mx_abs) {
     unsigned int m[2] = {0, 0};
     for (auto &s : c->slabs) {
         unsigned int t[2];
-        SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));
-        SQ_HIP(hipMemsetAsync(c->dmax, 0, 2 * sizeof(unsigned int), s.sA));
         SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane_floats(c), c->dacc,
-                                       c->dmax, s.sA));
+                                       c->dmax, c->dpart, s.sA));
         int rc = rank_allreduce(c, c->dmax, 2, sq::P2pRed::kMaxU32, s.sA);
         if (rc) return rc;
         SQ_HIP(hipMemcpyAsync(t, c->dmax, sizeof t, hipMemcpyDeviceToHost, s.sA));
@@ -1280,7 +1293,10 @@ int stab_rule(float &T, float &V, const float *M, const float *D, const float *A
 
 int phi4_frame(sq_ctx *c, int *stable) {
     const size_t plane = plane_floats(c);
-    int rc = phi4_join(c);
+    // one slab without an exchange: every launch of the frame is on stream A,
+    // so stream order replaces the joins around the set-up
+    const bool one_stream = c->slabs.size() == 1 && c->p.comm == SQ_COMM_NONE;
+    int rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;
     if (!c->stab_init) {  // the first frame's leader value and running max: the field itself
         rc = phi4_field_max(c, &c->stab_T, &c->stab_V);
@@ -1288,15 +1304,13 @@ int phi4_frame(sq_ctx *c, int *stable) {
         c->stab_init = true;
     }
     const size_t nrec = (size_t)sq::kStabSlots * (size_t)c->p.loops;
-    SQ_HIP(hipMemsetAsync(c->st_md, 0, sizeof(unsigned long long) * nrec, c->slabs[0].sA));
-    SQ_HIP(hipMemsetAsync(c->st_a, 0, sizeof(unsigned int) * nrec, c->slabs[0].sA));
+    SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, c->slabs[0].sA));  // records and guard flag
     for (auto &s : c->slabs) {  // frame-start snapshot, kept on device
         const size_t bytes = (size_t)s.nz * plane * sizeof(float);
         if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
         SQ_HIP(hipMemcpyAsync(s.snap, plane0(c, s, c->cur), bytes, hipMemcpyDeviceToDevice, s.sA));
     }
-    SQ_HIP(hipMemsetAsync(c->flag, 0, sizeof(int), c->slabs[0].sA));
-    rc = phi4_join(c);
+    rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;
     c->in_frame = true;
     c->frame_step0 = c->step;
@@ -1304,7 +1318,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     rc = phi4_steps(c, c->p.loops);
     c->in_frame = false;
     if (rc) return rc;
-    rc = phi4_join(c);
+    rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;
     Slab &s0 = c->slabs[0];
     if (per_rank(c->p.comm) && c->p.nranks > 1) {
@@ -1316,13 +1330,13 @@ int phi4_frame(sq_ctx *c, int *stable) {
         if (grp) SQ_NCCL(ncclGroupEnd());
         if (rc) return rc;
     }
-    int h = 0;
-    std::vector<unsigned long long> md(nrec);
-    std::vector<unsigned int> am(nrec);
-    SQ_HIP(hipMemcpyAsync(&h, c->flag, sizeof(int), hipMemcpyDeviceToHost, s0.sA));
-    SQ_HIP(hipMemcpyAsync(md.data(), c->st_md, sizeof(unsigned long long) * nrec, hipMemcpyDeviceToHost, s0.sA));
-    SQ_HIP(hipMemcpyAsync(am.data(), c->st_a, sizeof(unsigned int) * nrec, hipMemcpyDeviceToHost, s0.sA));
+    // one read-back of the records and the flag into pinned memory
+    SQ_HIP(hipMemcpyAsync(c->frame_host, c->frame_rec, c->frame_bytes, hipMemcpyDeviceToHost, s0.sA));
     SQ_HIP(hipStreamSynchronize(s0.sA));
+    const char *hb = static_cast<const char *>(c->frame_host);
+    const unsigned long long *md = reinterpret_cast<const unsigned long long *>(hb);
+    const unsigned int *am = reinterpret_cast<const unsigned int *>(hb + nrec * sizeof(unsigned long long));
+    const int h = *reinterpret_cast<const int *>(hb + nrec * (sizeof(unsigned long long) + sizeof(unsigned int)));
     const int L = c->p.loops;
     c->rec_M.assign(L, 0.f);
     c->rec_D.assign(L, 0.f);
@@ -1477,12 +1491,19 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->g_cand);
     (void)hipFree(c->g_flags);
     (void)hipFree(c->g_st);
-    (void)hipFree(c->flag);
+    if (c->frame_rec) {  // flag, st_md, st_a live in it
+        (void)hipFree(c->frame_rec);
+    } else {
+        (void)hipFree(c->flag);
+        (void)hipFree(c->st_md);
+        (void)hipFree(c->st_a);
+    }
+    if (c->frame_host) (void)hipHostFree(c->frame_host);
     (void)hipFree(c->dacc);
+    (void)hipFree(c->dpart);
+    (void)hipFree(c->dslice);
     (void)hipFree(c->dtune);
     (void)hipFree(c->dmax);
-    (void)hipFree(c->st_md);
-    (void)hipFree(c->st_a);
     if (c->qstream) (void)hipStreamDestroy(c->qstream);
     for (auto &e : c->evpool) {
         (void)hipEventDestroy(e.a);
@@ -1791,15 +1812,13 @@ int sq_moments(sq_ctx *c, double out[3]) {
     const size_t plane = plane_floats(c);
     out[0] = out[1] = out[2] = 0;
     for (auto &s : c->slabs) {
-        SQ_HIP(hipMemsetAsync(c->dacc, 0, 2 * sizeof(double), s.sA));  // same stream as the kernel:
-        SQ_HIP(hipMemsetAsync(c->dmax, 0, 2 * sizeof(unsigned int), s.sA));  // the null stream does not order non-blocking streams
         SQ_HIP(sq::phi4_moments_launch(plane0(c, s, c->cur), (long long)s.nz * (long long)plane,
-                                       c->dacc, c->dmax, s.sA));
+                                       c->dacc, c->dmax, c->dpart, s.sA));
         double acc[2];
         unsigned int mx;
+        SQ_HIP(hipMemcpyAsync(acc, c->dacc, sizeof acc, hipMemcpyDeviceToHost, s.sA));
+        SQ_HIP(hipMemcpyAsync(&mx, c->dmax, sizeof mx, hipMemcpyDeviceToHost, s.sA));
         SQ_HIP(hipStreamSynchronize(s.sA));
-        SQ_HIP(hipMemcpy(acc, c->dacc, sizeof acc, hipMemcpyDeviceToHost));
-        SQ_HIP(hipMemcpy(&mx, c->dmax, sizeof mx, hipMemcpyDeviceToHost));
         float fm;
         memcpy(&fm, &mx, sizeof fm);
         out[0] += acc[0];
@@ -1861,8 +1880,8 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     // per-frame collective of SURVEY.md §8e)
     const long long Lz = c->Lz;
     std::vector<double> S((size_t)Lz, 0.0);
-    double *d = nullptr;
-    SQ_HIP(hipMalloc(&d, sizeof(double) * (size_t)Lz));
+    if (!c->dslice) SQ_HIP(hipMalloc(&c->dslice, sizeof(double) * (size_t)Lz));
+    double *d = c->dslice;
     hipStream_t s0 = c->slabs[0].sA;
     hipError_t e = hipMemsetAsync(d, 0, sizeof(double) * (size_t)Lz, s0);
     for (auto &s : c->slabs) {
@@ -1872,14 +1891,10 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     }
     if (e == hipSuccess && per_rank(c->p.comm) && c->p.nranks > 1) {
         // disjoint z ranges, zeros elsewhere: the sum is exact in any order
-        if (int rc = rank_allreduce(c, d, (size_t)Lz, sq::P2pRed::kSumF64, s0)) {
-            (void)hipFree(d);
-            return rc;
-        }
+        if (int rc = rank_allreduce(c, d, (size_t)Lz, sq::P2pRed::kSumF64, s0)) return rc;
     }
+    if (e == hipSuccess) e = hipMemcpyAsync(S.data(), d, sizeof(double) * (size_t)Lz, hipMemcpyDeviceToHost, s0);
     if (e == hipSuccess) e = hipStreamSynchronize(s0);
-    if (e == hipSuccess) e = hipMemcpy(S.data(), d, sizeof(double) * (size_t)Lz, hipMemcpyDeviceToHost);
-    (void)hipFree(d);
     if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
     const double vol = (double)c->Lx * c->Ly * (double)Lz;
     for (int t = 0; t < n; ++t) {

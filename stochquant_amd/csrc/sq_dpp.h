@@ -1,5 +1,6 @@
 // sq_dpp.h -- wave-level helpers on DPP lane moves (no LDS round trips),
-// shared by the QM1D kernels (sq_qm1d.hip, sq_qm1d_gs.hip).
+// shared by the QM1D kernels (sq_qm1d.hip, sq_qm1d_gs.hip) and the phi^4
+// frame records (sq_phi4.hip).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -49,6 +50,21 @@ __device__ __forceinline__ int dpp_all_max_i(int v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ float dpp_f(float v, float id) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, id), __builtin_bit_cast(int, v),
+                                                                 CTRL, RM, BM, false));
+}
+__device__ __forceinline__ float dpp_all_max_f(float v) {  // wave maximum (no NaN inputs), wave-uniform
+    const float id = -__builtin_inff();
+    v = fmaxf(v, dpp_f<0x111, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x112, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x114, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x118, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x142, 0xa, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x143, 0xc, 0xf>(v, id));
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
 
 // lane l <- lane l-1 (wave_shr:1) / lane l+1 (wave_shl:1); the lane shifted
 // in from outside the wave keeps `id`

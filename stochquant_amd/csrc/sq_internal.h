@@ -75,10 +75,12 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
 // slab = local plane 0 (past the ghost zone)
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
-// Moments of a slab: acc[0] += sum phi, acc[1] += sum phi^2; acc_max[0] = max
-// |phi| (float bits), acc_max[1] = max phi (order-preserving bits, see
-// sq_phi4.hip ord_f32).  acc and acc_max must be zeroed by the caller.
-hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max,
+// Moments of a slab: acc = {sum phi, sum phi^2}, acc_max = {bits(max |phi|),
+// ord(max phi)} (order-preserving bits, sq_phi4.hip ord_f32), written, not
+// accumulated; part: kMomBlocks * 4 doubles of scratch.  Deterministic:
+// per-block partials folded in block order by a second one-block kernel.
+constexpr int kMomBlocks = 1024;
+hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max, double *part,
                                hipStream_t s);
 // Slice sums S(z) = sum_{x,y} phi(x,y,z) for z in [0,nz): out[z] (double); slab = local plane 0.
 hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double *out,

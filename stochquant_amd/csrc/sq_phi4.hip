@@ -21,6 +21,7 @@
 
 #include <algorithm>
 
+#include "sq_dpp.h"
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -156,32 +157,46 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
 // flag of tau_kernel.cl:119-133 and, per step, the record of the stability
 // heuristic (tau_kernel.cl:135-143): m = max phi', d = the
 // drift increment |phi' - phi - sigma xi| at the sites attaining m (the
-// largest one on ties), a = max |phi'|.
+// largest one on ties), a = max |phi'|.  mw: the wave's running maximum of
+// phi' (wave-uniform).
 struct FrameAcc {
     int bad;
     float m, d, a;
+    float mw;
 };
-__device__ __forceinline__ FrameAcc frame_acc() { return FrameAcc{0, -__builtin_inff(), 0.f, 0.f}; }
+__device__ __forceinline__ FrameAcc frame_acc() {
+    return FrameAcc{0, -__builtin_inff(), 0.f, 0.f, -__builtin_inff()};
+}
 
 __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float xi, float sig) {
     const float dn = fabsf(__builtin_fmaf(-sig, xi, o - c));
     f.d = o > f.m ? dn : (o == f.m ? fmaxf(f.d, dn) : f.d);
     f.m = fmaxf(f.m, o);
-    f.a = fmaxf(f.a, fabsf(o));
 }
 
 // The frame bookkeeping of one float4 of outputs o (inputs c, noise xi).
+// A site below the wave's running maximum mw can neither set nor tie the
+// step's maximum, so the per-site (m, d) update runs only when some lane's
+// float4 reaches mw (wave-uniform branch; on iid values a wave meets a new
+// maximum in about H(n) of its n planes): the lanes' (m, d) may then miss
+// sites below mw, but the wave's maximum key ord(m) << 32 | bits(d), all
+// that frame_flush keeps, is exact.  a and the guard flag take every site.
 template <bool NZ>
 __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
                                             const f32x4n &xi) {
     const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
     f.bad |= (int)(m >= A.clampv);
     if (A.st_md != nullptr) {
-        const float s = NZ ? A.sigq : 0.f;
-        stab_site(f, o.x, c.x, xi.a, s);
-        stab_site(f, o.y, c.y, xi.b, s);
-        stab_site(f, o.z, c.z, xi.c, s);
-        stab_site(f, o.w, c.w, xi.d, s);
+        f.a = fmaxf(f.a, m);
+        const float o4 = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
+        if (__ballot(o4 >= f.mw) != 0ull) {
+            const float s = NZ ? A.sigq : 0.f;
+            stab_site(f, o.x, c.x, xi.a, s);
+            stab_site(f, o.y, c.y, xi.b, s);
+            stab_site(f, o.z, c.z, xi.c, s);
+            stab_site(f, o.w, c.w, xi.d, s);
+            f.mw = dpp_all_max_f(f.m);
+        }
     }
 }
 
@@ -860,8 +875,10 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-__global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long long n4,
-                                                           double *acc, unsigned int *acc_max) {
+// Per-block partials (no atomics: 1024 blocks' double atomics on one address
+// serialised at one L2 channel, 57 us per 256^3 call), then one block folds
+// them in block order -- the same bits on every call.
+__global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long long n4, double *part) {
     double s1 = 0, s2 = 0;
     float mx = 0, mp = -__builtin_inff();
     const float4 *q = reinterpret_cast<const float4 *>(p);
@@ -896,10 +913,52 @@ __global__ __launch_bounds__(256) void phi4_moments_kernel(const float *p, long 
             tm = fmaxf(tm, shm[k]);
             tp = fmaxf(tp, shp[k]);
         }
-        atomicAdd(&acc[0], t1);
-        atomicAdd(&acc[1], t2);
-        atomicMax(acc_max, __float_as_uint(tm));
-        atomicMax(acc_max + 1, ord_f32(tp));
+        double *q = part + 4 * (size_t)blockIdx.x;
+        q[0] = t1;
+        q[1] = t2;
+        q[2] = (double)tm;
+        q[3] = (double)tp;
+    }
+}
+
+__global__ __launch_bounds__(256) void phi4_moments_final_kernel(const double *part, int nb, double *acc,
+                                                                 unsigned int *acc_max) {
+    double s1 = 0, s2 = 0, mx = 0, mp = -__builtin_inf();
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+        const double *q = part + 4 * (size_t)b;
+        s1 += q[0];
+        s2 += q[1];
+        mx = fmax(mx, q[2]);
+        mp = fmax(mp, q[3]);
+    }
+    __shared__ double sh[4][4];
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = fmax(mx, __shfl_xor(mx, o, 64));
+        mp = fmax(mp, __shfl_xor(mp, o, 64));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sh[w][0] = s1;
+        sh[w][1] = s2;
+        sh[w][2] = mx;
+        sh[w][3] = mp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t1 = 0, t2 = 0, tm = 0, tp = -__builtin_inf();
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+            t1 += sh[k][0];
+            t2 += sh[k][1];
+            tm = fmax(tm, sh[k][2]);
+            tp = fmax(tp, sh[k][3]);
+        }
+        acc[0] = t1;
+        acc[1] = t2;
+        acc_max[0] = __float_as_uint((float)tm);
+        acc_max[1] = ord_f32((float)tp);
     }
 }
 
@@ -1072,11 +1131,13 @@ hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, 
     return hipGetLastError();
 }
 
-hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max,
+hipError_t phi4_moments_launch(const float *slab, long long n, double *acc, unsigned int *acc_max, double *part,
                                hipStream_t s) {
     const long long n4 = n / 4;
-    const unsigned grid = (unsigned)std::min<long long>((n4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(phi4_moments_kernel, dim3(grid), dim3(256), 0, s, slab, n4, acc, acc_max);
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, kMomBlocks));
+    hipLaunchKernelGGL(phi4_moments_kernel, dim3(grid), dim3(256), 0, s, slab, n4, part);
+    hipLaunchKernelGGL(phi4_moments_final_kernel, dim3(1), dim3(256), 0, s, (const double *)part, (int)grid, acc,
+                       acc_max);
     return hipGetLastError();
 }
 
