@@ -181,21 +181,31 @@ __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float x
 // maximum in about H(n) of its n planes): the lanes' (m, d) may then miss
 // sites below mw, but the wave's maximum key ord(m) << 32 | bits(d), all
 // that frame_flush keeps, is exact.  a and the guard flag take every site.
+// bw (the fused kernel): the block's running maximum of this record in LDS,
+// raised by each wave that meets a new maximum of its own; the threshold is
+// then the larger of the two, still a value some site of the record attains,
+// so the block's key stays exact and a wave takes the per-site path about
+// 1 + H(n)/waves times instead of H(n).  Waves read it without
+// a barrier: any value read is a valid (monotone, attained) threshold.
 template <bool NZ>
 __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
-                                            const f32x4n &xi) {
+                                            const f32x4n &xi, float *bw = nullptr) {
     const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
     f.bad |= (int)(m >= A.clampv);
     if (A.st_md != nullptr) {
         f.a = fmaxf(f.a, m);
         const float o4 = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
-        if (__ballot(o4 >= f.mw) != 0ull) {
+        float t = f.mw;
+        if (bw != nullptr) t = fmaxf(t, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (__ballot(o4 >= t) != 0ull) {
             const float s = NZ ? A.sigq : 0.f;
             stab_site(f, o.x, c.x, xi.a, s);
             stab_site(f, o.y, c.y, xi.b, s);
             stab_site(f, o.z, c.z, xi.c, s);
             stab_site(f, o.w, c.w, xi.d, s);
             f.mw = dpp_all_max_f(f.m);
+            if (bw != nullptr && (threadIdx.x & 63) == 0)
+                __hip_atomic_fetch_max(bw, f.mw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 }
@@ -667,7 +677,7 @@ template <bool NZ, bool WIDE, bool FR, bool WH, int J>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, TbRun &R, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
-                                         FrameAcc &f2) {
+                                         FrameAcc &f2, float *bmx) {
     constexpr int sl = J, sp = (J + 2) % 3;  // slots of planes p and p-1
     __amdgpu_buffer_rsrc_t rs, rc;
     uint32_t ss = 0, sc = 0;
@@ -698,7 +708,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             rgt = from_right_lane(I1.row.x);
         }
         T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v);
-        if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa);
+        if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa, bmx);
         lds[sl][K.w][K.lane] = T2;
     } else {
         // the x-halo wave: step s at its 16 sites of plane p
@@ -726,7 +736,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         }
         // step s+1 reads step s's guarded output: always finite
         const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v);
-        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb);
+        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb, bmx + 1);
         if constexpr (WH) {
             bstore4<17>(K.rout, K.voff, o, (uint32_t)(p - 1 + A.gz) * K.pbytes);
         } else {
@@ -830,6 +840,11 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     }
     float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
     FrameAcc f1 = frame_acc(), f2 = frame_acc();  // steps s and s+1
+    __shared__ float bmx[2];                        // the block's running maxima of both records (frame_sites)
+    if constexpr (FR) {
+        if (threadIdx.x < 2) bmx[threadIdx.x] = -__builtin_inff();
+        __syncthreads();
+    }
     TbRun R;
     R.scur = (uint32_t)tb_pidx(A, K.z0 - 1) * K.pbytes;
     R.snext = (uint32_t)tb_pidx(A, K.z0) * K.pbytes;
@@ -837,11 +852,11 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     R.qzm = 0;  // plane z0-2: no step s+1 output there
     // three-plane queues unrolled three ways so no rotation moves are emitted
     for (int p = K.z0 - 1; p <= z1; p += 3) {
-        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2, bmx);
         if (p + 1 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2, bmx);
         if (p + 2 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2);
+        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2, bmx);
     }
     if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
         __shared__ uint64_t sk[kTbWaves + 1];
