@@ -170,6 +170,7 @@ struct sq_ctx {
     int cur = 0;
     int *flag = nullptr;
     bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
+    float *snap_next = nullptr;  // phi4_frame: the next fused launch writes its input here (Phi4StepArgs::snap)
     bool field_finite = true;  // every plane of the current field has been through the guard (or
                                // came from sq_init_field); false after a caller's upload / load
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
@@ -392,6 +393,8 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     const int nr = lo2 < hi2 ? 2 : 1, len = hi - lo;
     if (nr == 2 && hi2 - lo2 != len) return fail(SQ_E_STATE, "two-step launch: ranges of different lengths");
     sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
+    a.snap = c->snap_next;  // only a one-stream frame's first launch (phi4_frame)
+    c->snap_next = nullptr;
     // planes per block: pinned, or as many as make one round of tb_blocks
     // blocks (a ragged second round costs more than the deeper chunks), but
     // not fewer than 4 (a chunk recomputes 2 planes of the first step)
@@ -1305,10 +1308,17 @@ int phi4_frame(sq_ctx *c, int *stable) {
     }
     const size_t nrec = (size_t)sq::kStabSlots * (size_t)c->p.loops;
     SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, c->slabs[0].sA));  // records and guard flag
-    for (auto &s : c->slabs) {  // frame-start snapshot, kept on device
+    // frame-start snapshot, kept on device: a one-stream frame that starts
+    // with a fused pair has that launch store its input's interior (every
+    // site once, nontemporal), otherwise a device copy
+    const bool snap_in_kernel = one_stream && c->tbz > 0 && c->p.loops >= 2;
+    for (auto &s : c->slabs) {
         const size_t bytes = (size_t)s.nz * plane * sizeof(float);
         if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
-        SQ_HIP(hipMemcpyAsync(s.snap, plane0(c, s, c->cur), bytes, hipMemcpyDeviceToDevice, s.sA));
+        if (snap_in_kernel)
+            c->snap_next = s.snap;
+        else
+            SQ_HIP(hipMemcpyAsync(s.snap, plane0(c, s, c->cur), bytes, hipMemcpyDeviceToDevice, s.sA));
     }
     rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;
@@ -1317,6 +1327,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     const bool fin0 = c->field_finite;
     rc = phi4_steps(c, c->p.loops);
     c->in_frame = false;
+    c->snap_next = nullptr;
     if (rc) return rc;
     rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;

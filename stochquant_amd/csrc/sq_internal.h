@@ -40,6 +40,9 @@ struct Phi4StepArgs {
     // st_a + k*kStabSlots (u32 max of bits(max |phi'|)); DESIGN.md §7
     unsigned long long *st_md;
     unsigned int *st_a;
+    // frames (nullable): the frame's first fused launch also stores its input's
+    // interior planes here -- the rollback snapshot, without a copy kernel
+    float *snap;
 };
 constexpr int kStabSlots = 32;
 constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2): box_muller_q's missing factor (sq_rng.h)

@@ -123,7 +123,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 template <bool NZ>
 __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, float4 up, float4 dn,
                                                float4 zm, float4 zp, const f32x4n &xi,
-                                               const Phi4StepArgs &A, bool fin, f32x2 m2v) {
+                                               const Phi4StepArgs &A, bool fin, f32x2 m2v,
+                                               float *mpre = nullptr) {
     const f32x2 c0 = {c.x, c.y}, c1 = {c.z, c.w};
     // c.x + c.z and c.y + c.w as two single adds: formed as one v_pk_add they
     // share a register pair and take two v_mov to reach x0 / x1
@@ -147,6 +148,7 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
     const float cl = A.clampv;
     float4 o = make_float4(v0.x, v0.y, v1.x, v1.y);
     const float m = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)), fabsf(o.w));  // v_max3 + v_max
+    if (mpre != nullptr) *mpre = m;  // frames: max |phi'| before the guard (frame_sites)
     if (!fin || !(m < cl))
         o = make_float4(fmaxf(fminf(o.x, cl), -cl), fmaxf(fminf(o.y, cl), -cl), fmaxf(fminf(o.z, cl), -cl),
                         fmaxf(fminf(o.w, cl), -cl));
@@ -159,13 +161,18 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
 // drift increment |phi' - phi - sigma xi| at the sites attaining m (the
 // largest one on ties), a = max |phi'|.  mw: the wave's running maximum of
 // phi' (wave-uniform).
+// am: the running max of max |phi'| taken before the guard (finite inputs
+// only): the guard clamps to [-clamp, clamp], so after it max |phi'| is
+// min(am, clamp) and some site reached the clamp iff am >= clamp -- a and
+// bad follow from am at the flush, one v_max per float4 instead of six.
 struct FrameAcc {
     int bad;
     float m, d, a;
     float mw;
+    float am;
 };
 __device__ __forceinline__ FrameAcc frame_acc() {
-    return FrameAcc{0, -__builtin_inff(), 0.f, 0.f, -__builtin_inff()};
+    return FrameAcc{0, -__builtin_inff(), 0.f, 0.f, -__builtin_inff(), 0.f};
 }
 
 __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float xi, float sig) {
@@ -187,13 +194,20 @@ __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float x
 // so the block's key stays exact and a wave takes the per-site path about
 // 1 + H(n)/waves times instead of H(n).  Waves read it without
 // a barrier: any value read is a valid (monotone, attained) threshold.
+// pre: mpre is site_update4's pre-guard max |phi'| of o (finite inputs: no
+// NaN can hide from it), accumulated into am.
 template <bool NZ>
 __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
-                                            const f32x4n &xi, float *bw = nullptr) {
-    const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-    f.bad |= (int)(m >= A.clampv);
-    if (A.st_md != nullptr) {
+                                            const f32x4n &xi, float *bw = nullptr, bool pre = false,
+                                            float mpre = 0.f) {
+    if (pre) {
+        f.am = fmaxf(f.am, mpre);
+    } else {
+        const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+        f.bad |= (int)(m >= A.clampv);
         f.a = fmaxf(f.a, m);
+    }
+    if (A.st_md != nullptr) {
         const float o4 = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
         float t = f.mw;
         if (bw != nullptr) t = fmaxf(t, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -222,10 +236,11 @@ __device__ __forceinline__ uint32_t ord_f32(float v) {
 // every wave of the block must call it.
 __device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAcc &f, int rec, uint64_t *sk,
                                             uint32_t *sa) {
-    if (__ballot(f.bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    const bool bad = f.bad != 0 || f.am >= A.clampv;
+    if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     if (A.st_md == nullptr) return;
     uint64_t k = ((uint64_t)ord_f32(f.m) << 32) | __float_as_uint(f.d);
-    uint32_t a = __float_as_uint(f.a);
+    uint32_t a = __float_as_uint(fmaxf(f.a, fminf(f.am, A.clampv)));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t k2 = __shfl_xor(k, o, 64);
@@ -628,6 +643,8 @@ struct TbIn {
 };
 
 // Per-block constants of the march.
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
 struct TbCtx {
     size_t plane;
     uint32_t pbytes, qplane;
@@ -641,7 +658,7 @@ struct TbCtx {
     uint32_t qwrap;      // Lz_global * plane / 4: where the Philox quad base wraps
     f32x2 m2v;           // {m2, m2}, pinned in VGPRs (site_update4)
     int swrap_at;        // WH, periodic: the plane p at which plane p+1's input wraps to local 0
-    int z0, w, lane;
+    int z0, z1, w, lane;
     bool outw;
 };
 
@@ -707,8 +724,16 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             lft = from_left_lane(I1.row.w);
             rgt = from_right_lane(I1.row.x);
         }
-        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v);
-        if constexpr (FR) frame_sites<NZ>(A, f1, T2, I1.row, xa, bmx);
+        float mp1;
+        T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v, &mp1);
+        if constexpr (FR) {
+            frame_sites<NZ>(A, f1, T2, I1.row, xa, bmx, A.fin != 0, mp1);
+            // the frame's snapshot: each output row's input at its owned planes, once
+            if (A.snap != nullptr && K.outw && p + 1 >= K.z0 && p + 1 < K.z1)
+                __builtin_nontemporal_store(
+                    (f32x4v){I2.row.x, I2.row.y, I2.row.z, I2.row.w},
+                    reinterpret_cast<f32x4v *>(reinterpret_cast<char *>(A.snap) + (size_t)(p + 1) * K.pbytes + K.voff));
+        }
         lds[sl][K.w][K.lane] = T2;
     } else {
         // the x-halo wave: step s at its 16 sites of plane p
@@ -735,8 +760,9 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
             rgt = from_right_lane(T1.x);
         }
         // step s+1 reads step s's guarded output: always finite
-        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v);
-        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb, bmx + 1);
+        float mp2;
+        const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v, &mp2);
+        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb, bmx + 1, true, mp2);
         if constexpr (WH) {
             bstore4<17>(K.rout, K.voff, o, (uint32_t)(p - 1 + A.gz) * K.pbytes);
         } else {
@@ -778,6 +804,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     const int r0 = A.zlo + (zk / A.nzr) * A.zstep;  // this chunk's range
     K.z0 = r0 + (zk % A.nzr) * A.zc;
     const int z1 = min(K.z0 + A.zc, r0 + A.zlen);
+    K.z1 = z1;
     K.plane = (size_t)Lx * (size_t)Ly;
     K.pbytes = (uint32_t)(K.plane * sizeof(float));
     K.qplane = (uint32_t)(K.plane >> 2);

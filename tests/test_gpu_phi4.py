@@ -720,3 +720,31 @@ def test_stability_rule_quiet_on_stable_frames(gpu, oracle_mod, bm_tables):
     assert np.array_equal(st["M"], M) and np.array_equal(st["D"], D) and np.array_equal(st["A"], A)
     assert st["T"] == T1 and st["V"] == V1
     assert np.array_equal(got, out)
+
+
+@pytest.mark.parametrize("shape", [(256, 16, 12), (512, 8, 9)])
+@pytest.mark.parametrize("loops", [2, 3, 5])
+def test_frame_snapshot_from_first_fused_launch(gpu, oracle_mod, shape, loops):
+    """A one-stream frame's rollback snapshot is stored by its first fused
+    launch (Phi4StepArgs::snap, DESIGN.md §7): after stable frames have moved
+    the field between the ping-pong buffers, an unstable frame (a clamp hit
+    and a NaN) still restores the frame-start field bit for bit, odd frame
+    lengths (a fused pair, then per-step launches) included."""
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    with _lat(shape, loops=loops) as L:
+        assert "tb2" in L.kernel_name
+        L.upload(phi0)
+        for _ in range(3):
+            start = L.download()
+            assert L.run_frame()
+            assert not np.array_equal(L.download(), start)
+        bad = L.download()
+        bad[1, 2, 3] = np.float32(5e3)
+        bad[-1, -1, -1] = np.float32("nan")
+        L.upload(bad)
+        assert not L.run_frame()
+        back = L.download()
+        ok = ~np.isnan(bad)
+        assert np.array_equal(back[ok], bad[ok]) and np.isnan(back[-1, -1, -1])
+        L.upload(_init(oracle_mod, shape, amp=0.2, seed=5))
+        assert L.run_frame()
