@@ -190,6 +190,7 @@ struct sq_ctx {
     void *frame_rec = nullptr;
     void *frame_host = nullptr;
     size_t frame_bytes = 0;
+    bool frame_rec_zero = true;  // frame_rec is (or is queued to be) all zero: the next frame skips its memset
     unsigned long long frame_step0 = 0;  // Philox step of the frame's first step
     bool stab_init = false;              // T, V set from the field at the first frame
     float stab_T = 0, stab_V = 0;        // carried across frames, never rolled back (as lrgEl / lrgVl)
@@ -1307,7 +1308,9 @@ int phi4_frame(sq_ctx *c, int *stable) {
         c->stab_init = true;
     }
     const size_t nrec = (size_t)sq::kStabSlots * (size_t)c->p.loops;
-    SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, c->slabs[0].sA));  // records and guard flag
+    if (!c->frame_rec_zero)  // records and guard flag (normally cleared behind the previous read-back)
+        SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, c->slabs[0].sA));
+    c->frame_rec_zero = false;
     // frame-start snapshot, kept on device: a one-stream frame that starts
     // with a fused pair has that launch store its input's interior (every
     // site once, nontemporal), otherwise a device copy
@@ -1343,6 +1346,9 @@ int phi4_frame(sq_ctx *c, int *stable) {
     }
     // one read-back of the records and the flag into pinned memory
     SQ_HIP(hipMemcpyAsync(c->frame_host, c->frame_rec, c->frame_bytes, hipMemcpyDeviceToHost, s0.sA));
+    // clear the records for the next frame behind the read-back (stream order), off its start
+    SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, s0.sA));
+    c->frame_rec_zero = true;
     SQ_HIP(hipStreamSynchronize(s0.sA));
     const char *hb = static_cast<const char *>(c->frame_host);
     const unsigned long long *md = reinterpret_cast<const unsigned long long *>(hb);
