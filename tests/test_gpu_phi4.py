@@ -748,3 +748,30 @@ def test_frame_snapshot_from_first_fused_launch(gpu, oracle_mod, shape, loops):
         assert np.array_equal(back[ok], bad[ok]) and np.isnan(back[-1, -1, -1])
         L.upload(_init(oracle_mod, shape, amp=0.2, seed=5))
         assert L.run_frame()
+
+
+@pytest.mark.parametrize("path", ["mono", "rccl"])
+def test_stable_frames_equal_raw_steps(gpu, oracle_mod, monkeypatch, path):
+    """Frames that stay stable advance the field exactly as the same number of
+    raw steps on the same noise counters: the frame instances of the kernels
+    (guard flag, stability records, the snapshot store of the first fused
+    launch) must not touch the trajectory (scripts/diag_frame_vs_steps.py)."""
+    from stochquant_amd import unique_id
+    shape = (256, 8, 16)
+    phi0 = _init(oracle_mod, shape)
+
+    def run(frames):
+        kw = {}
+        if path == "rccl":
+            monkeypatch.setenv("SQ_GHOST", "4")
+            kw = dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id())
+        with _lat(shape, loops=6, **kw) as L:
+            L.upload(phi0)
+            if frames:
+                for _ in range(3):
+                    assert L.run_frame()
+            else:
+                L.step(18)
+            return L.download()
+
+    assert np.array_equal(run(True), run(False))
