@@ -156,7 +156,11 @@ int sq_run_frame(sq_ctx *ctx, int *stable);
 
 /* PHI4: raw Langevin steps without frame control (the bench's hot path). */
 int sq_step(sq_ctx *ctx, int nsteps);
-/* PHI4 field I/O of this process' slab(s): nz_local*Ly*Lx floats, z slowest. */
+/* PHI4 field I/O of this process' slab(s): nz_local*Ly*Lx floats, z slowest.
+ * In multi-rank contexts (SQ_COMM_RCCL / SQ_COMM_P2P, nranks > 1) sq_upload_field,
+ * sq_init_field and sq_load_field are collective like sq_step: every rank calls
+ * them before its next step call, which agrees across the ranks on whether the
+ * field (and so every rank's ghost planes) is known to be guarded. */
 int sq_upload_field(sq_ctx *ctx, const float *phi, size_t count);
 int sq_download_field(sq_ctx *ctx, float *phi, size_t count);
 /* PHI4: phi = amp * Philox normal(seed, stream 2, site), generated on device. */
@@ -216,7 +220,9 @@ int sq_get_params(sq_ctx *ctx, sq_params *out);
  * is a NumPy .npy float32 array of shape (nz, Ly, Lx); <path>.json holds the
  * lattice dims, z0, the Philox step counter, Δτ and the seed.  Replaces the
  * reference's text end/start file (tauhost.c:91-173,562-581) for 3-D fields.
- * sq_load_field with restore_counters != 0 also restores step and Δτ. */
+ * sq_load_field with restore_counters != 0 also restores step and Δτ, and the
+ * frame state carried across frames (the stability heuristic's T, V and the Δτ
+ * controller's stable-frame count; files without it restart that state). */
 int sq_save_field(sq_ctx *ctx, const char *path);
 int sq_load_field(sq_ctx *ctx, const char *path, int restore_counters);
 

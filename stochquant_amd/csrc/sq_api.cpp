@@ -173,6 +173,8 @@ struct sq_ctx {
     float *snap_next = nullptr;  // phi4_frame: the next fused launch writes its input here (Phi4StepArgs::snap)
     bool field_finite = true;  // every plane of the current field has been through the guard (or
                                // came from sq_init_field); false after a caller's upload / load
+    bool fin_sync = false;     // multi-rank: field_finite changed locally; the next step call
+                               // agrees on it across ranks first (ghost planes come from neighbours)
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
     int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
     bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
@@ -812,6 +814,19 @@ int phi4_steps_impl(sq_ctx *c, int n) {
     }
     if (c->p.comm == SQ_COMM_P2P && !c->p2p_ready)
         return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
+    if (c->fin_sync) {  // one rank's unguarded upload makes the others' ghost planes unguarded too
+        c->fin_sync = false;
+        if (per_rank(c->p.comm) && c->p.nranks > 1) {
+            hipStream_t st = c->slabs[0].sA;
+            double v = c->field_finite ? 0.0 : 1.0;
+            SQ_HIP(hipMemcpyAsync(c->dtune, &v, sizeof v, hipMemcpyHostToDevice, st));
+            int rc = rank_allreduce(c, c->dtune, 1, sq::P2pRed::kMaxF64, st);
+            if (rc) return rc;
+            SQ_HIP(hipMemcpyAsync(&v, c->dtune, sizeof v, hipMemcpyDeviceToHost, st));
+            SQ_HIP(hipStreamSynchronize(st));
+            c->field_finite = v == 0.0;
+        }
+    }
     if (c->g_auto && !c->g_tuned) {
         int rc = phi4_autotune(c, n);
         if (rc) return rc;
@@ -862,9 +877,14 @@ int create_phi4(sq_ctx *c) {
         // inside [-clamp, clamp] to be finite or +-inf, never NaN: bound the drift
         const double cl = p.clamp, h = p.deltatau;
         const double drift = 12.0 * cl + std::fabs(p.m2) * cl + std::fabs(p.lambda) / 6.0 * cl * cl * cl;
+        // (float)clamp squared finite too: with lambda = 0, clamp^2 = inf would make
+        // fma(lam/6, phi^2, m2) = 0 * inf = NaN at |phi| = clamp
+        const float clf = (float)cl;
         if (!std::isfinite(cl) || !(cl > 0) || !std::isfinite(p.m2) || !std::isfinite(p.lambda) ||
-            !std::isfinite(p.C) || !(h * drift + cl + 16.0 * sqrt(2.0 * h) * std::fabs(p.C) < 1e30))
-            return fail(SQ_E_ARG, "PHI4 parameters must be finite with dtau * drift(clamp) < 1e30");
+            !std::isfinite(p.C) || !std::isfinite(clf * clf) ||
+            !(h * drift + cl + 16.0 * sqrt(2.0 * h) * std::fabs(p.C) < 1e30))
+            return fail(SQ_E_ARG, "PHI4 parameters must be finite with clamp^2 finite in fp32 and "
+                                  "dtau * drift(clamp) < 1e30");
     }
     if (const char *e = getenv("SQ_ROWS")) {  // tuning override of the rows per lane
         const int r = atoi(e), rs = 64 / c->geom.qx;
@@ -1741,6 +1761,30 @@ int sq_phi4_stability(sq_ctx *c, double state[2], int *fired_step, float *M, flo
     return SQ_OK;
 }
 
+}  // extern "C"
+
+namespace sq {
+int frame_state_get(const sq_ctx *c, FrameState *fs) {
+    if (!c || !fs) return fail(SQ_E_ARG, "null argument");
+    fs->T = c->stab_T;
+    fs->V = c->stab_V;
+    fs->init = c->stab_init ? 1 : 0;
+    fs->stab_cnt = c->stab_cnt;
+    return SQ_OK;
+}
+int frame_state_set(sq_ctx *c, const FrameState &fs) {
+    if (!c) return fail(SQ_E_ARG, "null argument");
+    if (fs.stab_cnt < 0) return fail(SQ_E_ARG, "stab_cnt must be >= 0");
+    c->stab_T = fs.T;
+    c->stab_V = fs.V;
+    c->stab_init = fs.init != 0;
+    c->stab_cnt = fs.stab_cnt;
+    return SQ_OK;
+}
+}  // namespace sq
+
+extern "C" {
+
 int sq_phi4_set_stability(sq_ctx *c, double T, double V) {
     if (!c) return fail(SQ_E_ARG, "null context");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
@@ -1785,6 +1829,7 @@ int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {
         off += (size_t)s.nz * plane;
     }
     c->field_finite = false;  // the caller's values (NaN / inf / beyond the clamp allowed) meet the full guard
+    c->fin_sync = true;
     return SQ_OK;
 }
 
@@ -1817,6 +1862,7 @@ int sq_init_field(sq_ctx *c, float amp) {
         SQ_HIP(sq::phi4_init_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
                                     (uint32_t)(c->p.seed >> 32), amp, s.sA));
     c->field_finite = std::isfinite(amp) && std::fabs(amp) * 8.0f < (float)c->p.clamp;
+    c->fin_sync = true;
     return phi4_join(c);
 }
 

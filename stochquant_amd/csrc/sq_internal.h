@@ -11,6 +11,24 @@ namespace sq {
 // Sets the thread-local message returned by sq_last_error(); returns code.
 int set_error(int code, const std::string &msg);
 
+}  // namespace sq
+
+struct sq_ctx;
+
+namespace sq {
+
+// Frame-control state a phi^4 checkpoint carries besides the field and the
+// counters (sq_io.cpp): the stability heuristic's carried T and V and whether
+// they were set, and the dtau controller's stable-frame count
+// (tauhost.c:523-541).  Not part of the C ABI.
+struct FrameState {
+    float T, V;
+    int init;
+    int stab_cnt;
+};
+int frame_state_get(const sq_ctx *c, FrameState *fs);
+int frame_state_set(sq_ctx *c, const FrameState &fs);
+
 // ---------------------------------------------------------------- PHI4 ----
 // One slab lives in a padded buffer of (nz + 2*gz) planes of Lx*Ly floats, z
 // slowest: padded plane gz + zl holds local plane zl, for zl in [-gz, nz+gz).

@@ -108,6 +108,15 @@ long long json_int(const std::string &j, const char *key, bool *found) {
     return *found ? strtoll(j.c_str() + p + k.size(), nullptr, 10) : 0;
 }
 
+// Unsigned 64-bit fields (seed, step): strtoull, so values >= 2^63 round-trip
+// (strtoll would saturate them to LLONG_MAX).
+unsigned long long json_uint(const std::string &j, const char *key, bool *found) {
+    const std::string k = std::string("\"") + key + "\":";
+    const size_t p = j.find(k);
+    *found = p != std::string::npos;
+    return *found ? strtoull(j.c_str() + p + k.size(), nullptr, 10) : 0ull;
+}
+
 double json_dbl(const std::string &j, const char *key, bool *found) {
     const std::string k = std::string("\"") + key + "\":";
     const size_t p = j.find(k);
@@ -134,13 +143,17 @@ static int save_field(sq_ctx *ctx, const char *path) {
     double dtau = 0;
     sq_get_step(ctx, &step);
     sq_get_dtau(ctx, &dtau);
+    sq::FrameState fs{};
+    if (sq::frame_state_get(ctx, &fs) != SQ_OK) return io_fail("frame state unavailable");
     const std::string jpath = std::string(path) + ".json";
     FILE *fp = fopen(jpath.c_str(), "w");
     if (!fp) return io_fail("cannot write " + jpath);
     fprintf(fp,
             "{\"format\": \"stochquant-phi4-slab\", \"version\": 1, \"dims\": [%lld, %lld, %lld], "
-            "\"z0\": %lld, \"nz\": %lld, \"step\": %llu, \"dtau\": %.17g, \"seed\": %llu}\n",
-            P.dims[0], P.dims[1], P.dims[2], z0, nz, step, dtau, P.seed);
+            "\"z0\": %lld, \"nz\": %lld, \"step\": %llu, \"dtau\": %.17g, \"seed\": %llu, "
+            "\"stab_init\": %d, \"stab_T\": %.9g, \"stab_V\": %.9g, \"stab_cnt\": %d}\n",
+            P.dims[0], P.dims[1], P.dims[2], z0, nz, step, dtau, P.seed, fs.init, (double)fs.T, (double)fs.V,
+            fs.stab_cnt);
     return fclose(fp) == 0 ? SQ_OK : io_fail("cannot write " + jpath);
 }
 
@@ -169,15 +182,27 @@ static int load_field(sq_ctx *ctx, const char *path, int restore_counters) {
     std::string j;
     const bool have_meta = read_text(jpath, &j);
     if (restore_counters && !have_meta) return io_fail("cannot read " + jpath);
-    long long step = 0, jz0 = 0, jnz = 0;
+    unsigned long long step = 0;
+    long long jz0 = 0, jnz = 0;
     double dtau = 0;
+    // frame-control state (version-1 files written before round 3 lack it:
+    // the heuristic then restarts from the field at the next frame)
+    sq::FrameState fs{0.f, 0.f, 0, 0};
+    bool have_fs = false;
     if (have_meta) {
         bool f1, f2, f3, f4, f5;
-        step = json_int(j, "step", &f1);
+        step = json_uint(j, "step", &f1);
         dtau = json_dbl(j, "dtau", &f2);
         jz0 = json_int(j, "z0", &f3);
         jnz = json_int(j, "nz", &f4);
-        const unsigned long long seed = (unsigned long long)json_int(j, "seed", &f5);
+        const unsigned long long seed = json_uint(j, "seed", &f5);
+        bool g1, g2, g3, g4;
+        fs.init = (int)json_int(j, "stab_init", &g1);
+        fs.T = (float)json_dbl(j, "stab_T", &g2);
+        fs.V = (float)json_dbl(j, "stab_V", &g3);
+        fs.stab_cnt = (int)json_int(j, "stab_cnt", &g4);
+        have_fs = g1 && g2 && g3 && g4;
+        if (have_fs && fs.stab_cnt < 0) return io_fail("checkpoint stab_cnt must be >= 0");
         long long dims[3];
         if (!f1 || !f2 || !f3 || !f4 || !f5 || !json_dims(j, dims)) return io_fail("incomplete checkpoint metadata " + jpath);
         if (dims[0] != P.dims[0] || dims[1] != P.dims[1] || dims[2] != P.dims[2])
@@ -194,8 +219,13 @@ static int load_field(sq_ctx *ctx, const char *path, int restore_counters) {
     int rc = sq_upload_field(ctx, f.data(), f.size());
     if (rc) return rc;
     if (restore_counters) {
-        sq_set_step(ctx, (unsigned long long)step);
+        sq_set_step(ctx, step);
         sq_set_dtau(ctx, dtau);
+        // the stability heuristic's T, V and the dtau controller's count carry
+        // across frames: a resume continues them
+        if (!have_fs) fs = sq::FrameState{0.f, 0.f, 0, 0};
+        rc = sq::frame_state_set(ctx, fs);
+        if (rc) return rc;
     }
     return SQ_OK;
 }

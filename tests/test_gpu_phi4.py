@@ -543,6 +543,38 @@ def test_checkpoint_roundtrip_resumes_noise_bitwise(gpu, oracle_mod, tmp_path):
             L.load(tmp_path / "ck.npy")
 
 
+def test_checkpoint_large_seed_and_frame_state(gpu, oracle_mod, tmp_path):
+    """Seeds >= 2^63 round-trip through the checkpoint metadata (unsigned
+    parse), and a resume carries the frame state across: the stability
+    heuristic's T and V and the dtau controller's stable-frame count, so
+    frames after the load equal the uninterrupted run's (field, dtau, T, V)."""
+    import json
+    shape, seed = (256, 8, 12), 0xFEDCBA9876543210
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    with _lat(shape, loops=4, seed=seed, dtau=0.01) as L:
+        L.upload(phi0)
+        for _ in range(7):
+            assert L.run_frame()
+        L.save(tmp_path / "ck.npy")
+        st0 = L.stability()
+        for _ in range(9):                  # crosses the 11-stable-frames dtau growth
+            assert L.run_frame()
+        full, d_full, st_full = L.download(), L.dtau, L.stability()
+    meta = json.loads((tmp_path / "ck.npy.json").read_text())
+    assert meta["seed"] == seed and meta["stab_cnt"] == 7 and meta["stab_init"] == 1
+    assert np.float32(meta["stab_T"]) == np.float32(st0["T"]) and np.float32(meta["stab_V"]) == np.float32(st0["V"])
+    with _lat(shape, loops=4, seed=seed, dtau=0.01) as L:
+        L.load(tmp_path / "ck.npy")
+        st = L.stability(0)
+        assert st["T"] == st0["T"] and st["V"] == st0["V"]
+        for _ in range(9):
+            assert L.run_frame()
+        assert L.dtau == d_full and d_full > 0.01
+        st = L.stability()
+        assert st["T"] == st_full["T"] and st["V"] == st_full["V"]
+        assert np.array_equal(L.download(), full)
+
+
 def test_slice_correlator_across_slabs(gpu, oracle_mod):
     """The zero-momentum correlator of a decomposed lattice (loopback slabs;
     RCCL self-exchange = the all-reduce code path of the multi-rank case) equals
