@@ -22,7 +22,17 @@ all ranks / max over ranks of that wall time.  `roofline.achieved` = 8
 algorithmic bytes per site update x the updates of one launch
 / the mean launch duration from one hipEvent pair on the kernel's own stream
 around the K timed steps (`frac_kernel`); `frac_wall` is the same bytes over
-the wall time behind `value`.  Prints ONE JSON line (rank 0).
+the wall time behind `value`; `frac_real` is the real HBM bytes of a launch
+(the committed rocprofv3 PMC summary of this command) over the same launch time
+-- the physical roofline, which the algorithmic figure (8 B per update, the
+fused kernel moving the field once per two updates) cannot show.
+
+Also in the line: `multi_rank_check` (stochquant_amd/verify.py: every rank's
+slab after a fixed check protocol against the golden digests of a single-GPU
+run of the same global lattice -- "pass" / "fail"), and, in the default N = 1
+run, `c3_512`: BASELINE configs[2] (512^3, HBM-resident) measured the same way
+in the same invocation, with its own roofline and CPU sample.  Prints ONE JSON
+line (rank 0).
 """
 import argparse
 import json
@@ -64,6 +74,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target wall time of the CPU sample")
     ap.add_argument("--no-profile-events", action="store_true",
                     help="no hipEvents in the timed region (roofline.achieved then uses wall time)")
+    ap.add_argument("--no-check", action="store_true", help="skip the multi_rank_check protocol")
+    ap.add_argument("--corrupt-rank", type=int, default=-1,
+                    help="(tests) flip one value of this rank's slab before its check digest")
+    ap.add_argument("--no-c3", action="store_true", help="skip the 512^3 (configs[2]) sub-record of the default run")
+    ap.add_argument("--cpu-seconds-c3", type=float, default=8.0, help="target wall time of the 512^3 CPU sample")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks and their process group, print each rank's slab and deep-halo "
                          "schedule, touch no GPU (tests the multi-rank launch path on a CPU host)")
@@ -188,31 +203,11 @@ def pmc_record(L, nranks, kernel):
     return None, None
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if a.gpus > 1 and "RANK" not in os.environ:
-        sys.exit(spawn_ranks(a.gpus))
-    rank = int(os.environ.get("RANK", "0"))
-    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
-    a.gpus = world
-    import torch
+def make_lattice(a, shape, world, rank, local):
+    """The bench's lattice for this rank: one periodic slab at N = 1, RCCL z-slabs
+    at N > 1 (or the transport --comm names)."""
+    from stochquant_amd import Phi4Lattice, connect_p2p, unique_id
     import torch.distributed as dist
-    from stochquant_amd import Phi4Lattice, connect_p2p, unique_id, _lib
-    _lib.load()  # fail loudly if the HIP library is missing
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
-        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    if a.dry_run:
-        dry_run(a, world, rank, local, dist)
-        if world > 1:
-            dist.destroy_process_group()
-        return
-    torch.cuda.set_device(local)
-    L = a.size
-    shape = (L, L, L) if a.strong else (L, L, L * world)
     kw = dict(dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local)
     if a.comm == "p2p":
         lat = Phi4Lattice(shape, comm="p2p", nranks=world, rank=rank, **kw)
@@ -230,8 +225,16 @@ def main():
         lat = Phi4Lattice(shape, comm="loopback", nslabs=a.slabs, **kw)
     else:
         lat = Phi4Lattice(shape, **kw)
-    slab_path = world > 1 or a.comm != "auto"
-    lat.init_field(0.1)
+    return lat, (world > 1 or a.comm != "auto")
+
+
+def measure(a, lat, world, slab_path):
+    """Settle, warm-up, EXACTLY a.steps timed steps (barrier + device sync on both
+    sides, max over ranks), then the roofline pass: the same steps again with one
+    hipEvent pair on the step-kernel stream.  Returns (wall seconds, perf,
+    settle_ms, settle_steps)."""
+    import torch
+    import torch.distributed as dist
 
     def barrier():
         if world > 1:
@@ -292,12 +295,12 @@ def main():
         tt = torch.tensor([t], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
-    # sanity: the field stayed finite and bounded (no guard hits)
-    m = lat.moments()
-    sites_local = lat.nz_local * L * L
-    total_updates = float(shape[0] * shape[1] * shape[2]) * a.steps
-    value = total_updates / t
-    nslabs = a.slabs if (world == 1 and a.comm == "loopback") else 1
+    return t, perf, settle_ms, settle_steps
+
+
+def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
+    """The bench line's roofline object for the dominant (step) kernel."""
+    value = float(sites_local * world) * a.steps / t if not a.strong else None
     launches = max(1, perf["kernel_launches"])
     spl = perf["steps"] * nslabs / launches          # steps per launch, measured (2 = two-step fused)
     if perf["step_kernel_launches"] > 0:
@@ -308,8 +311,111 @@ def main():
         step_ms = t * 1e3 / a.steps
     launch_ms = step_ms * spl
     achieved = BYTES_PER_SITE * sites_local / (step_ms * 1e-3) / 1e9
-    achieved_wall = BYTES_PER_SITE * value / 1e9
     kname = lat.kernel_name
+    rec, rec_path = pmc_record(L, world, kname) if not slab_path else (None, None)
+    fused = "tb2" in kname and perf.get("fused_steps", 0) >= 0.5 * perf["steps"]
+    r = {
+        # the fused kernel moves the field once per two updates
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "frac_kernel": round(achieved / HBM_PEAK_GBPS, 4),
+        "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time",
+        "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
+        "traffic_source": (f"cached: {rec_path}, rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this "
+                           f"bench command (not measured inside this run)") if rec else None,
+        "kernel": kname,
+        "timing": "hipEvent pair on the kernel stream around a second pass of the same K steps right "
+                  "after the wall-timed region (region mean)"
+                  if perf["step_kernel_launches"] > 0 else "wall clock",
+        "steps_per_launch": round(spl, 3),
+        "kernel_launches_timed": perf["kernel_launches"],
+        "algorithmic_bytes_per_launch": round(BYTES_PER_SITE * sites_local * spl),
+        "avg_launch_us": round(launch_ms * 1e3, 3),
+        "avg_step_us": round(step_ms * 1e3, 3),
+        # the least HBM traffic a launch can have (one read + one write
+        # of the field) and the rate it moved at
+        "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_local,
+        "hbm_min_GBps": round(BYTES_PER_SITE * sites_local / (launch_ms * 1e-3) / 1e9, 1),
+    }
+    if rec:
+        # headroom the algorithmic figure cannot show (it counts 8 B per update,
+        # the fused kernel moves the field once per two): the real HBM bytes of
+        # a launch (PMC) over this run's launch time, the per-SIMD VALU issue
+        # utilisation and the launch busy fraction of the committed counters
+        tb = rec.get("hbm_bytes_per_launch")
+        if tb:
+            r["real_GBps"] = round(tb / (launch_ms * 1e-3) / 1e9, 1)
+            r["frac_real"] = round(tb / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        for k in ("valu_util_simd", "valu_util_method", "busy_fraction", "busy_source", "pmc_kernel_us"):
+            if rec.get(k) is not None:
+                r[k] = rec[k]
+    return r, value, fused
+
+
+def cpu_baseline_c3(L, dtau, target_s):
+    try:
+        return cpu_baseline(L, dtau, target_s)
+    except Exception as e:  # the GPU record stands without it
+        return {"error": str(e)[:200]}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    a.gpus = world
+    import torch
+    import torch.distributed as dist
+    from stochquant_amd import _lib, verify
+    _lib.load()  # fail loudly if the HIP library is missing
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.dry_run:
+        dry_run(a, world, rank, local, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    torch.cuda.set_device(local)
+    L = a.size
+    shape = (L, L, L) if a.strong else (L, L, L * world)
+    lat, slab_path = make_lattice(a, shape, world, rank, local)
+    lat.init_field(0.1)
+    t, perf, settle_ms, settle_steps = measure(a, lat, world, slab_path)
+    # sanity: the field stayed finite and bounded (no guard hits)
+    m = lat.moments()
+    sites_local = lat.nz_local * L * L
+    total_updates = float(shape[0] * shape[1] * shape[2]) * a.steps
+    value = total_updates / t
+    nslabs = a.slabs if (world == 1 and a.comm == "loopback") else 1
+    rl, _, fused = roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local)
+    achieved_wall = BYTES_PER_SITE * value / 1e9
+    rl["frac_wall"] = round(achieved_wall / HBM_PEAK_GBPS, 4)
+    rl["achieved_wall"] = round(achieved_wall, 1)
+    # self-check (verify.py): the check protocol's slab digests against the
+    # golden ones of a single-GPU run of the same global lattice, every rank
+    check = "skipped"
+    if not a.no_check and a.dtau == verify.CHECK_PARAMS["dtau"]:
+        d = verify.run_protocol(lat, corrupt=(rank == a.corrupt_rank))
+        digests = [None] * world
+        if world > 1:
+            dist.all_gather_object(digests, d)
+        else:
+            digests = [d]
+        check = verify.check(digests, shape, world)
+    ghost = lat.ghost[0] if slab_path else None
+    schedule = lat.schedule if slab_path else None
+    kname = lat.kernel_name
+    nz_local = lat.nz_local
+    lat.close()
     out = None
     if rank == 0:
         copy = None
@@ -320,9 +426,14 @@ def main():
                 copy = round(g.value, 1)
         except Exception:
             copy = None
-        rec, rec_path = pmc_record(L, world, kname) if not slab_path else (None, None)
-        # the fused two-step kernel carries most steps (slab paths: all but the odd tails)
-        fused = "tb2" in kname and perf.get("fused_steps", 0) >= 0.5 * perf["steps"]
+        cfg_idx = {256: 1, 512: 2}.get(L)
+        if a.strong:
+            workload = f"phi^4 3-D Langevin step, {L}^3 fp32 split over {world} GPU(s) (BASELINE configs[4], strong)"
+        elif world > 1:
+            workload = f"phi^4 3-D Langevin step, {L}^3 fp32 per GPU, weak-scaled z-slabs (BASELINE configs[3])"
+        else:
+            workload = (f"phi^4 3-D Langevin step, {L}^3 fp32 on one GPU"
+                        + (f" (BASELINE configs[{cfg_idx}])" if cfg_idx is not None else ""))
         out = {
             "metric": METRIC,
             "value": value,
@@ -339,48 +450,21 @@ def main():
             "dtype": "fp32",
             "data": "synthetic (phi0 = 0.1*Philox normal, seed 0x5EED)",
             "config": {
-                "workload": f"phi^4 3-D Langevin step, {L}^3 fp32 per GPU (BASELINE configs[1]"
-                            f"{'' if world == 1 else ', weak-scaled slabs = configs[3]'})" if not a.strong else
-                            f"phi^4 3-D Langevin step, {L}^3 fp32 split over {world} GPU(s) (BASELINE configs[4], strong)",
+                "workload": workload,
                 "lattice": list(shape),
-                "per_gpu": [L, L, lat.nz_local],
+                "per_gpu": [L, L, nz_local],
                 "dtau": a.dtau, "m2": 1.0, "lambda": 1.0,
-                "ghost_depth": lat.ghost[0] if slab_path else None,
-                "block_schedule": lat.schedule if slab_path else None,
+                "ghost_depth": ghost,
+                "block_schedule": schedule,
                 "parallelism": "single GPU, one stream" if not slab_path else
                                f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else 'rccl'}), halo exchange on "
                                f"stream B, interior on stream A",
             },
-            "roofline": {
-                # the fused kernel moves the field once per two updates and is issue-bound
-                # (PMC: profiles/r02/); the per-step kernel at 512^3+ is HBM-bound
-                "bound": "valu" if fused else "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "frac_kernel": round(achieved / HBM_PEAK_GBPS, 4),
-                "frac_wall": round(achieved_wall / HBM_PEAK_GBPS, 4),
-                "achieved_wall": round(achieved_wall, 1),
-                "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time",
-                "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
-                "traffic_source": (f"cached: {rec_path}, rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this "
-                                   f"bench command (not measured inside this run)") if rec else None,
-                "valu_issue_frac": rec.get("valu_issue_frac") if rec else None,
-                "kernel": kname,
-                "timing": "hipEvent pair on the kernel stream around a second pass of the same K steps right "
-                          "after the wall-timed region (region mean)"
-                          if perf["step_kernel_launches"] > 0 else "wall clock",
-                "steps_per_launch": round(spl, 3),
-                "kernel_launches_timed": perf["kernel_launches"],
-                "algorithmic_bytes_per_launch": round(BYTES_PER_SITE * sites_local * spl),
-                "avg_launch_us": round(launch_ms * 1e3, 3),
-                "avg_step_us": round(step_ms * 1e3, 3),
-                # the least HBM traffic a launch can have (one read + one write
-                # of the field) and the rate it moved at
-                "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_local,
-                "hbm_min_GBps": round(BYTES_PER_SITE * sites_local / (launch_ms * 1e-3) / 1e9, 1),
-            },
+            "roofline": rl,
+            "multi_rank_check": check,
+            "multi_rank_check_protocol": (f"init 0.1*normal, step counter 0, {verify.CHECK_STEPS} steps; every "
+                                          f"rank's slab digest vs the golden single-GPU run "
+                                          f"(stochquant_amd/golden_slabs.json)"),
             "hbm_copy_peak_GBps": copy,
             "field_check": {"rms": (m["sum2"] / sites_local) ** 0.5, "maxabs": m["maxabs"]},
         }
@@ -388,7 +472,28 @@ def main():
             out["cpu_baseline"] = cpu_baseline(L, a.dtau, a.cpu_seconds)
         else:
             out["cpu_baseline"] = None
-    lat.close()
+    # config C3 (BASELINE configs[2], 512^3 on one GPU) in the same invocation:
+    # the same settle, warm-up and --steps, its own roofline and CPU sample
+    if world == 1 and not a.strong and a.comm == "auto" and L == 256 and not a.no_c3:
+        L3 = 512
+        lat3, _ = make_lattice(a, (L3, L3, L3), 1, 0, local)
+        lat3.init_field(0.1)
+        t3, perf3, settle3, ssteps3 = measure(a, lat3, 1, False)
+        sites3 = L3 ** 3
+        rl3, value3, _ = roofline(a, lat3, L3, 1, False, t3, perf3, 1, sites3)
+        rl3["frac_wall"] = round(BYTES_PER_SITE * value3 / 1e9 / HBM_PEAK_GBPS, 4)
+        m3 = lat3.moments()
+        lat3.close()
+        out["c3_512"] = {
+            "config": {"workload": "phi^4 3-D Langevin step, 512^3 fp32 on one GPU (BASELINE configs[2], "
+                                   "HBM-resident: 2 x 512 MiB > the 256 MiB Infinity Cache)",
+                       "lattice": [L3, L3, L3], "dtau": a.dtau, "m2": 1.0, "lambda": 1.0},
+            "value": value3, "unit": "site-updates/s", "steps": a.steps, "warmup": a.warmup,
+            "settle_ms": round(settle3, 1), "settle_steps": ssteps3, "ms_per_step": t3 * 1e3 / a.steps,
+            "roofline": rl3,
+            "field_check": {"rms": (m3["sum2"] / sites3) ** 0.5, "maxabs": m3["maxabs"]},
+            "cpu_baseline": None if a.no_cpu_baseline else cpu_baseline_c3(L3, a.dtau, a.cpu_seconds_c3),
+        }
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -268,6 +268,10 @@ int sq_device_count(int *n);
 int sq_selftest_normals(int device, unsigned long long seed, unsigned int stream,
                         unsigned long long quad0, unsigned long long step, float *out, size_t nquads);
 int sq_selftest_dpp(int device, float *out64x2);
+/* DPP cross-wave stress: mode 0 every wave rotates (wave_ror/rol:1), 1 even waves
+ * run the records' row_shr/row_bcast wave-max scan while odd waves rotate, 2 every
+ * wave does both, 3 as 1 without row_bcast; errs64[lane] = wrong rotated values. */
+int sq_selftest_dpp_mix(int device, int mode, int blocks, int iters, unsigned int *errs64);
 int sq_selftest_philox(int device, const unsigned int ctr[4], const unsigned int key[2], unsigned int out[4]);
 int sq_copy_bandwidth(int device, size_t bytes, int iters, double *gbps);
 /* The serial order's draws of one full launch from `seed` on the device:

@@ -31,7 +31,7 @@ def main():
     # (N, dt, dtau, potID, loops): taumain.py presets' shapes and the C1-like chain
     shapes = [(100, 0.1, 0.002, 3, 1000), (200, 0.1, 0.002, 3, 200), (1000, 0.05, 0.0005, 0, 1000),
               (3072, 0.05, 0.0005, 0, 200)]
-    if a.ordering == "jacobi" and not a.no_cpu and not a.no_c1:
+    if a.ordering == "jacobi" and not a.no_c1:
         shapes.append((32768, 1.0, 0.01, 0, 1000))  # config C1
     for N, dt, dtau, pot, loops in shapes:
         f0 = 0.1 * np.random.default_rng(1).standard_normal(N)

@@ -1,0 +1,1 @@
+bash scripts/r03_frames_diag.sh && bash scripts/r03_pipe_ab.sh

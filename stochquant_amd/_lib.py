@@ -142,6 +142,8 @@ SIGNATURES = {
     "sq_selftest_normals": (ctypes.c_int, [ctypes.c_int, ctypes.c_ulonglong, ctypes.c_uint,
                                            ctypes.c_ulonglong, ctypes.c_ulonglong, _F, ctypes.c_size_t]),
     "sq_selftest_dpp": (ctypes.c_int, [ctypes.c_int, _F]),
+    "sq_selftest_dpp_mix": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(ctypes.c_uint)]),
     "sq_selftest_philox": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint), ctypes.POINTER(ctypes.c_uint),
                                           ctypes.POINTER(ctypes.c_uint)]),
     "sq_copy_bandwidth": (ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, _D]),

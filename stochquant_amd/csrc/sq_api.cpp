@@ -98,7 +98,7 @@ struct Peer {  // a rank's buffers as this process addresses them
 
 struct P2pBlob {  // sq_p2p_handle's output
     unsigned int magic, version;
-    int rank, nranks, Lx, Ly, gpad, pad;
+    int rank, nranks, Lx, Ly, gpad, loops, gz, gauto;  // gz / gauto: active ghost depth, timed pick
     long long Lz, coll_cap;
     unsigned long long seed;
     hipIpcMemHandle_t stage, mbox, coll;
@@ -136,6 +136,9 @@ struct sq_ctx {
     int qcur = 0;
     sq::Qm1dState *qst = nullptr;
     double *qscr[3] = {nullptr, nullptr, nullptr};  // N > kQm1dRegMaxN: fs, xs, ds of Qm1dArgs
+    // N <= kQm1dRegMaxN, Jacobi frames: the precomputed tables of Qm1dArgs (om, xi, tcl, dd)
+    double *qom = nullptr, *qdd = nullptr;
+    float *qxi = nullptr, *qtcl = nullptr;
     double omega = 0;
     long runs = 0;
     int lrgEl = 0;
@@ -1239,6 +1242,22 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     a.k0 = (uint32_t)c->p.seed;
     a.k1 = (uint32_t)(c->p.seed >> 32);
     a.tick = c->step;
+    const bool tables = c->N <= sq::kQm1dRegMaxN;
+    if (tables) {  // the field-independent work of the frame, grid-wide ahead of the chain (qm1d_prep_launch)
+        const size_t L = (size_t)c->p.loops, nq4 = (size_t)((c->N + 3) & ~3);
+        if (!c->qom) {
+            SQ_HIP(hipMalloc(&c->qom, sizeof(double) * (L + 1)));
+            SQ_HIP(hipMalloc(&c->qxi, sizeof(float) * L * nq4));
+            if (c->p.pot == 3) {
+                SQ_HIP(hipMalloc(&c->qtcl, sizeof(float) * L * (size_t)(c->N + 2)));
+                SQ_HIP(hipMalloc(&c->qdd, sizeof(double) * L * (size_t)c->N));
+            }
+        }
+        a.om = c->qom;
+        a.xi = c->qxi;
+        a.tcl = c->qtcl;
+        a.dd = c->qdd;
+    }
     sq::Qm1dState st{};
     st.omega_in = c->omega;
     st.lrgEl = c->lrgEl;
@@ -1247,6 +1266,7 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     EvPair *e = nullptr;
     int rc = ev_begin(c, c->qstream, &e);
     if (rc) return rc;
+    if (tables) SQ_HIP(sq::qm1d_prep_launch(a, c->qstream));
     SQ_HIP(sq::qm1d_frame_launch(a, c->qstream));
     if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
     SQ_HIP(hipMemcpyAsync(&st, c->qst, sizeof st, hipMemcpyDeviceToHost, c->qstream));
@@ -1520,6 +1540,10 @@ int sq_destroy(sq_ctx *c) {
     }
     (void)hipFree(c->qst);
     for (double *q : c->qscr) (void)hipFree(q);
+    (void)hipFree(c->qom);
+    (void)hipFree(c->qdd);
+    (void)hipFree(c->qxi);
+    (void)hipFree(c->qtcl);
     for (double *q : {c->g_xi, c->g_om, c->g_xc, c->g_hist_buf, c->g_nfp}) (void)hipFree(q);
     (void)hipFree(c->g_w1);
     (void)hipFree(c->g_w2);
@@ -2016,6 +2040,9 @@ int sq_p2p_handle(sq_ctx *c, unsigned char out[SQ_P2P_HANDLE_BYTES]) {
     b.Lx = c->Lx;
     b.Ly = c->Ly;
     b.gpad = c->gpad;
+    b.loops = c->p.loops;
+    b.gz = c->gz;
+    b.gauto = c->g_auto ? 1 : 0;
     b.Lz = c->Lz;
     b.coll_cap = (long long)c->coll_cap;
     b.seed = c->p.seed;
@@ -2044,6 +2071,11 @@ int sq_p2p_connect(sq_ctx *c, const unsigned char *handles, int nranks) {
         if (b.Lx != c->Lx || b.Ly != c->Ly || b.Lz != c->Lz || b.gpad != c->gpad ||
             b.coll_cap != (long long)c->coll_cap || b.seed != c->p.seed)
             return fail(SQ_E_ARG, "rank " + std::to_string(q) + " was created for a different lattice, ghost depth or seed");
+        // the exchanges move gz planes and the frame collectives loops records:
+        // ranks that disagree would hang in a wait or fold mismatched records
+        if (b.loops != c->p.loops || b.gz != c->gz || b.gauto != (c->g_auto ? 1 : 0))
+            return fail(SQ_E_ARG, "rank " + std::to_string(q) + " has different loops (" + std::to_string(b.loops) +
+                                      "), active ghost depth (" + std::to_string(b.gz) + ") or ghost tuning (SQ_GHOST)");
     }
     DeviceGuard g(c->dev);
     for (int q = 0; q < nranks; ++q) {
@@ -2102,6 +2134,25 @@ int sq_selftest_dpp(int device, float *out64x2) {
     hipError_t e = sq::selftest_dpp_launch(d, nullptr);
     if (e == hipSuccess) e = hipMemcpy(out64x2, d, 128 * sizeof(float), hipMemcpyDeviceToHost);
     (void)hipFree(d);
+    if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
+    return SQ_OK;
+}
+
+int sq_selftest_dpp_mix(int device, int mode, int blocks, int iters, unsigned int *errs64) {
+    if (!errs64 || mode < 0 || mode > 3 || blocks < 1 || blocks > 65536 || iters < 1)
+        return fail(SQ_E_ARG, "bad dpp_mix arguments");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(SQ_E_NODEV, "no HIP device");
+    DeviceGuard g(device);
+    unsigned *d = nullptr;
+    float *sink = nullptr;
+    SQ_HIP(hipMalloc(&d, 64 * sizeof(unsigned)));
+    hipError_t e = hipMalloc(&sink, 1024 * sizeof(float));
+    if (e == hipSuccess) e = hipMemset(d, 0, 64 * sizeof(unsigned));
+    if (e == hipSuccess) e = sq::selftest_dpp_mix_launch(mode, blocks, iters, d, sink, nullptr);
+    if (e == hipSuccess) e = hipMemcpy(errs64, d, 64 * sizeof(unsigned), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    (void)hipFree(sink);
     if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
     return SQ_OK;
 }

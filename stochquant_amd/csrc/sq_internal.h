@@ -128,6 +128,15 @@ struct Qm1dArgs {
     const double *f, *x, *xx0;  // frame-start state (N)
     double *nf, *nx, *nxx0;     // state after the frame (N)
     double *fs, *xs, *ds;       // N > kQm1dRegMaxN only: f ping-pong, X' and drift-check scratch (N each)
+    // N <= kQm1dRegMaxN: the field-independent work of the frame, precomputed
+    // grid-wide (qm1d_prep_launch) so the per-step chain keeps only the field
+    // arithmetic: om[j] = omega at the start of step j (loops + 1), xi[j*nq4 + i]
+    // the site normals (nq4 = N rounded up to 4), and for potID 3
+    // tcl[j*(N+2) + i+1] = the float tanhf of x_cl(i a; om[j]) for i = -1..N and
+    // dd[j*N + i] = ddPot(x_cl(i a; om[j]))
+    double *om;
+    float *xi, *tcl;
+    double *dd;
     Qm1dState *st;
     int N, pot, loops, runs;
     double a, a2, h, sig, sigw, kconst;
@@ -139,6 +148,9 @@ int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant:
 constexpr int kQm1dMaxN = 1024 * 64;
 constexpr int kQm1dRegMaxN = 4096;  // register-resident frame kernel up to here; beyond, f ping-pong + scan scratch
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
+// The precomputed tables of a register-kernel frame (N <= kQm1dRegMaxN), on the
+// same stream ahead of qm1d_frame_launch; a.om / a.xi (/ a.tcl, a.dd) sized as above.
+hipError_t qm1d_prep_launch(const Qm1dArgs &a, hipStream_t s);
 
 // QM1D in the reference's serial order (sq_qm1d_gs.hip)
 struct Qm1dGsState {
@@ -186,6 +198,7 @@ hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long
                                    uint32_t stream, unsigned long long step, uint32_t k0,
                                    uint32_t k1, hipStream_t s);
 hipError_t selftest_dpp_launch(float *out, hipStream_t s);
+hipError_t selftest_dpp_mix_launch(int mode, int blocks, int iters, unsigned *errs, float *sink, hipStream_t s);
 hipError_t selftest_philox_launch(const uint32_t *ck, uint32_t *out, hipStream_t s);
 hipError_t selftest_libm_launch(int fn, const float *x, float *y, long long n, hipStream_t s);
 hipError_t selftest_bm_tables_launch(float *t, hipStream_t s);

@@ -64,8 +64,19 @@ __device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off,
     const f32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, off, soff, LAUX);
     return make_float4(v.x, v.y, v.z, v.w);
 }
+// Always with soffset 0 (an inline constant), never an SGPR: a 16-byte VMEM
+// store reads its data VGPRs after issue, and a VALU write of the first of
+// them right behind the store can land first -- on gfx950 the last four lanes
+// of every 16 then store the new value (found in round 3: the frame kernels'
+// first output component, lanes 12-15 / 28-31 / 44-47 / 60-63 of one row in a
+// few launches).  The compiler inserts the wait state for
+// this hazard only when soffset is not a register
+// (GCNHazardRecognizer::createsVALUHazard), so plane offsets go into the VGPR
+// offset; tests/test_isa_hazards.py checks the built code object for the
+// pattern.
 template <int AUX = 0>
-__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v, uint32_t soff = 0) {
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+    const uint32_t soff = 0;
     const f32x4v w = {v.x, v.y, v.z, v.w};
     __builtin_amdgcn_raw_buffer_store_b128(w, r, off, soff, AUX);
 }
@@ -159,20 +170,22 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
 // flag of tau_kernel.cl:119-133 and, per step, the record of the stability
 // heuristic (tau_kernel.cl:135-143): m = max phi', d = the
 // drift increment |phi' - phi - sigma xi| at the sites attaining m (the
-// largest one on ties), a = max |phi'|.  mw: the wave's running maximum of
-// phi' (wave-uniform).
-// am: the running max of max |phi'| taken before the guard (finite inputs
-// only): the guard clamps to [-clamp, clamp], so after it max |phi'| is
-// min(am, clamp) and some site reached the clamp iff am >= clamp -- a and
-// bad follow from am at the flush, one v_max per float4 instead of six.
+// largest one on ties), mw = the wave's running maximum of phi'
+// (wave-uniform).  am: the running max |phi'| -- taken before the guard where
+// the inputs are known finite (site_update4's mpre: no NaN can hide from it),
+// after the guard otherwise; either way the guard flag is am >= clamp (the
+// guard clamps to [-clamp, clamp], so some site reached the clamp iff the
+// maximum did) and max |phi'| after the guard is min(am, clamp).  One
+// accumulator for both forms: round 2 kept the post-guard flag and maximum in
+// two more, and the compiler selected between their addresses through 12
+// bytes of private memory per lane.
 struct FrameAcc {
-    int bad;
-    float m, d, a;
+    float m, d;
     float mw;
     float am;
 };
 __device__ __forceinline__ FrameAcc frame_acc() {
-    return FrameAcc{0, -__builtin_inff(), 0.f, 0.f, -__builtin_inff(), 0.f};
+    return FrameAcc{-__builtin_inff(), 0.f, -__builtin_inff(), 0.f};
 }
 
 __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float xi, float sig) {
@@ -187,7 +200,7 @@ __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float x
 // float4 reaches mw (wave-uniform branch; on iid values a wave meets a new
 // maximum in about H(n) of its n planes): the lanes' (m, d) may then miss
 // sites below mw, but the wave's maximum key ord(m) << 32 | bits(d), all
-// that frame_flush keeps, is exact.  a and the guard flag take every site.
+// that frame_flush keeps, is exact.  am (guard flag, max |phi'|) takes every site.
 // bw (the fused kernel): the block's running maximum of this record in LDS,
 // raised by each wave that meets a new maximum of its own; the threshold is
 // then the larger of the two, still a value some site of the record attains,
@@ -195,18 +208,13 @@ __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float x
 // 1 + H(n)/waves times instead of H(n).  Waves read it without
 // a barrier: any value read is a valid (monotone, attained) threshold.
 // pre: mpre is site_update4's pre-guard max |phi'| of o (finite inputs: no
-// NaN can hide from it), accumulated into am.
+// NaN can hide from it), accumulated into am; otherwise the guarded o's.
 template <bool NZ>
 __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
                                             const f32x4n &xi, float *bw = nullptr, bool pre = false,
                                             float mpre = 0.f) {
-    if (pre) {
-        f.am = fmaxf(f.am, mpre);
-    } else {
-        const float m = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-        f.bad |= (int)(m >= A.clampv);
-        f.a = fmaxf(f.a, m);
-    }
+    const float mo = pre ? mpre : fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+    f.am = fmaxf(f.am, mo);
     if (A.st_md != nullptr) {
         const float o4 = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
         float t = f.mw;
@@ -236,11 +244,11 @@ __device__ __forceinline__ uint32_t ord_f32(float v) {
 // every wave of the block must call it.
 __device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAcc &f, int rec, uint64_t *sk,
                                             uint32_t *sa) {
-    const bool bad = f.bad != 0 || f.am >= A.clampv;
+    const bool bad = f.am >= A.clampv;
     if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     if (A.st_md == nullptr) return;
     uint64_t k = ((uint64_t)ord_f32(f.m) << 32) | __float_as_uint(f.d);
-    uint32_t a = __float_as_uint(fmaxf(f.a, fminf(f.am, A.clampv)));
+    uint32_t a = __float_as_uint(fminf(f.am, A.clampv));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t k2 = __shfl_xor(k, o, 64);
@@ -764,7 +772,8 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v, &mp2);
         if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb, bmx + 1, true, mp2);
         if constexpr (WH) {
-            bstore4<17>(K.rout, K.voff, o, (uint32_t)(p - 1 + A.gz) * K.pbytes);
+            // the plane offset in the VGPR offset, soffset 0: see bstore4
+            bstore4<17>(K.rout, K.voff + (uint32_t)(p - 1 + A.gz) * K.pbytes, o);
         } else {
             const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
             bstore4<17>(ws, K.voff, o);
@@ -886,6 +895,296 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2, bmx);
     }
     if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
+        __shared__ uint64_t sk[kTbWaves + 1];
+        __shared__ uint32_t sa[kTbWaves + 1];
+        frame_flush(A, f1, 0, sk, sa);
+        frame_flush(A, f2, 1, sk, sa);
+    }
+}
+
+// ------------------------------------------- pipelined two-step fusion ----
+// phi4_tb2_kernel's block and work split (one 256-site x-segment of kTbRows
+// output rows of a z-chunk; row wave w holds row y0-1+w; S > 1: the x-halo
+// wave w = kTbWaves), with the loads decoupled from their use:
+//   * a row wave loads only ITS OWN row of each input plane (waves 0 and
+//     kTbWaves-1 also the row beyond, y0-2 / y0+9), one plane iteration
+//     before the plane is needed (plane k+2 is issued in iteration k and first
+//     read in iteration k+1), so the fetch overlaps a whole iteration of Philox
+//     and stencil work instead of the few instructions between a load and its
+//     use; in-plane y-neighbours come from an LDS ring of input planes, which
+//     replaces the y-halo loads (3 loads per wave and plane -> 1);
+//   * one barrier per iteration, at its end: iteration k publishes input plane
+//     k+1 (in_lds) and step s of plane k (t_lds) and reads only what iteration
+//     k-1 published, so step s+1 of plane k-1 follows step s of plane k with no
+//     barrier between them.  Two slots per ring suffice: a slot is rewritten
+//     one barrier after the iteration that last read it.
+// Iteration k (z0-1 <= k <= z1): A = step s at plane k (T(k)), B = step s+1 at
+// plane k-1 (rows y0..y0+7, k > z0), the same site_update4 calls with the same
+// operands as phi4_tb2_kernel, so the result is bit-identical to two single
+// steps.  Registers: own input rows of planes k-1..k+2 (I[4]) and T(k-2..k)
+// (T[4]) by plane index mod 4, so the march is unrolled four ways and nothing
+// rotates.
+constexpr int kTpRows = kTbWaves + 2;  // in_lds rows: y0-2 .. y0+9
+constexpr uint32_t kTpOob = 0x80000000u;  // a buffer offset past every descriptor's range (< 2^31 B): dropped
+
+struct TpRun {
+    uint32_t s2, s1;  // WH: byte offsets (in the padded input) of planes k+2 and k+1
+    uint32_t qz, qzm; // Philox quad bases of planes k and k-1
+};
+
+// Advance the per-plane scalars from k to k+1.
+template <bool WH>
+__device__ __forceinline__ void tp_advance(const Phi4StepArgs &A, const TbCtx &K, TpRun &R, int k) {
+    R.qzm = R.qz;
+    const uint32_t q = R.qz + K.qplane;
+    R.qz = q == K.qwrap ? 0u : q;
+    if constexpr (WH) {
+        R.s1 = R.s2;
+        R.s2 = k + 3 == K.swrap_at ? (uint32_t)A.gz * K.pbytes : R.s2 + K.pbytes;
+    }
+}
+
+// One plane iteration of a row wave.
+template <bool NZ, bool WIDE, bool FR, bool WH, int J>
+__device__ __forceinline__ void tp_row(const Phi4StepArgs &A, const TbCtx &K, TpRun &R, int k, bool xrow,
+                                       uint32_t vxr, int xslot, float4 (&I)[4], float4 (&T)[4], float4 (&X)[2],
+                                       float (&E)[2], float4 (*in_lds)[kTpRows][64], float4 (*t_lds)[kTbWaves][64],
+                                       float (*tx)[kTbWaves][2], FrameAcc &f1, FrameAcc &f2, float *bmx) {
+    constexpr int im = J, ic = (J + 1) & 3, ip = (J + 2) & 3, in2 = (J + 3) & 3;  // planes k-1, k, k+1, k+2
+    constexpr int tc = J, tm = (J + 3) & 3, tmm = (J + 2) & 3;                    // T(k), T(k-1), T(k-2)
+    constexpr int sc = J & 1, sn = (J + 1) & 1;  // ring slots of plane k / T(k) and of plane k+1 / T(k-1)
+    const bool more = k < K.z1;                  // planes k+2 (rows) and k+1 (edges) are inputs of the chunk
+    __amdgpu_buffer_rsrc_t r2, r1;
+    uint32_t o2 = 0, o1 = 0;
+    if constexpr (WH) {
+        r2 = r1 = K.rin;
+        o2 = R.s2;
+        o1 = R.s1;
+    } else {
+        r2 = plane_rsrc(A.in, tb_pidx(A, k + 2), K.plane, K.pbytes);
+        r1 = plane_rsrc(A.in, tb_pidx(A, k + 1), K.plane, K.pbytes);
+    }
+    // 1. prefetch plane k+2 (own row; waves 0 / 9 the row beyond) and, S > 1,
+    //    plane k+1's site just outside the segment (lane 0 / 63).  Every
+    //    vector-memory op of the march is issued unconditionally, the ones with
+    //    nothing to do at an out-of-range offset (the buffer unit drops them), so
+    //    every path has the same op sequence and the compiler's vmcnt waits
+    //    stay exact: the wait for plane k+1 leaves plane k+2 in flight.
+    I[in2] = bload4(r2, more ? K.voff : kTpOob, o2);
+    X[sc] = bload4(r2, more ? vxr : kTpOob, o2);
+    if constexpr (WIDE) E[sn] = bload1(r1, more ? K.vex : kTpOob, o1);
+    // 2. plane k+1 has arrived (issued one iteration ago): publish it for the
+    //    y-neighbour reads of iteration k+1, and, frames, snapshot it
+    in_lds[sn][K.w + 1][K.lane] = I[ip];
+    if (xrow) in_lds[sn][xslot][K.lane] = X[sn];
+    if constexpr (FR) {  // each output row's input at its owned planes, once, nontemporal
+        const bool sv = A.snap != nullptr && K.outw && k + 1 >= K.z0 && k + 1 < K.z1;
+        bstore4<2>(plane_rsrc(A.snap, k + 1, K.plane, K.pbytes), sv ? K.voff : kTpOob, I[ip]);
+    }
+    // 3. A: step s at plane k
+    const f32x4n xa = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
+    const float4 up = in_lds[sc][K.w][K.lane], dn = in_lds[sc][K.w + 2][K.lane];
+    float lft, rgt;
+    if constexpr (WIDE) {
+        lft = from_left_lane_or(I[ic].w, E[sc]);
+        rgt = from_right_lane_or(I[ic].x, E[sc]);
+    } else {
+        lft = from_left_lane(I[ic].w);
+        rgt = from_right_lane(I[ic].x);
+    }
+    float mp1;
+    T[tc] = site_update4<NZ>(I[ic], lft, rgt, up, dn, I[im], I[ip], xa, A, A.fin != 0, K.m2v, &mp1);
+    if constexpr (FR) frame_sites<NZ>(A, f1, T[tc], I[ic], xa, bmx, A.fin != 0, mp1);
+    t_lds[sc][K.w][K.lane] = T[tc];
+    // 4. B: step s+1 at plane k-1 from T(k-2), T(k-1), T(k) and T(k-1)'s
+    //    y-neighbours, published in iteration k-1
+    const bool bw = K.outw && k > K.z0;
+    float4 o = T[tc];  // stored at an out-of-range offset unless bw
+    if (bw) {
+        const f32x4n xb = tb_noise<NZ>(A, R.qzm, K.qoff, K.slo1, K.shi1);
+        const float4 bu = t_lds[sn][K.w - 1][K.lane], bd = t_lds[sn][K.w + 1][K.lane];
+        float bl, br;
+        if constexpr (WIDE) {
+            const float2 e = *reinterpret_cast<const float2 *>(&tx[sn][K.w][0]);  // one broadcast LDS read
+            bl = from_left_lane_or(T[tm].w, e.x);
+            br = from_right_lane_or(T[tm].x, e.y);
+        } else {
+            bl = from_left_lane(T[tm].w);
+            br = from_right_lane(T[tm].x);
+        }
+        float mp2;
+        o = site_update4<NZ>(T[tm], bl, br, bu, bd, T[tmm], T[tc], xb, A, true, K.m2v, &mp2);
+        if constexpr (FR) frame_sites<NZ>(A, f2, o, T[tm], xb, bmx + 1, true, mp2);
+    }
+    if constexpr (WH) {
+        bstore4<17>(K.rout, bw ? K.voff + (uint32_t)(k - 1 + A.gz) * K.pbytes : kTpOob, o);  // soffset 0: bstore4
+    } else {
+        const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, k - 1 + A.gz, K.plane, K.pbytes);
+        bstore4<17>(ws, bw ? K.voff : kTpOob, o);
+    }
+    __syncthreads();
+    tp_advance<WH>(A, K, R, k);
+}
+
+// One plane iteration of the x-halo wave (S > 1): step s at its 16 sites of
+// plane k from the centres in C[] (planes k-1..k+2 by index mod 4) and plane
+// k's in-plane neighbours NB[sc] (xm, xp, ym, yp); plane k+1's are loaded here.
+// Its own loop (phi4_tb2p_kernel), so its registers do not add to the row waves'.
+template <bool NZ, bool WH, int J>
+__device__ __forceinline__ void tp_xhalo(const Phi4StepArgs &A, const TbCtx &K, TpRun &R, int k, float (&C)[4],
+                                         float4 (&NB)[2], float (*tx)[kTbWaves][2]) {
+    constexpr int im = J, ic = (J + 1) & 3, ip = (J + 2) & 3, in2 = (J + 3) & 3;
+    constexpr int sc = J & 1, sn = (J + 1) & 1;
+    {
+        const bool more = k < K.z1;
+        __amdgpu_buffer_rsrc_t r2, r1;
+        uint32_t o2 = 0, o1 = 0;
+        if constexpr (WH) {
+            r2 = r1 = K.rin;
+            o2 = R.s2;
+            o1 = R.s1;
+        } else {
+            r2 = plane_rsrc(A.in, tb_pidx(A, k + 2), K.plane, K.pbytes);
+            r1 = plane_rsrc(A.in, tb_pidx(A, k + 1), K.plane, K.pbytes);
+        }
+        C[in2] = bload1(r2, more ? K.voff : kTpOob, o2);
+        NB[sn] = make_float4(bload1(r1, more ? K.vex : kTpOob, o1), bload1(r1, more ? K.vx2 : kTpOob, o1),
+                             bload1(r1, more ? K.vm : kTpOob, o1), bload1(r1, more ? K.vp : kTpOob, o1));
+    }
+    const f32x4n n = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
+    // lanes 0..7 hold x0-1 (component 3 of its quad), 8..15 x0+256 (component 0)
+    const float xi = K.lane >= 8 ? n.a : n.d;
+    const float t = tb_site(C[ic], NB[sc].x, NB[sc].y, NB[sc].z, NB[sc].w, C[im], C[ip], xi, A, NZ);
+    if (K.lane < 16) tx[sc][(K.lane & 7) + 1][K.lane >> 3] = t;
+    __syncthreads();
+    tp_advance<WH>(A, K, R, k);
+}
+
+template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
+__global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
+__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
+    const int yb = lb % A.nyg, rest = lb / A.nyg;
+    const int xs = WIDE ? rest % A.nxseg : 0, zk = WIDE ? rest / A.nxseg : rest;
+    const int Lx = A.Lx, Ly = A.Ly;
+    const int x0 = 256 * xs;
+    TbCtx K;
+    K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    K.lane = threadIdx.x & 63;
+    K.outw = K.w >= 1 && K.w <= kTbRows;
+    const int r0 = A.zlo + (zk / A.nzr) * A.zstep;
+    K.z0 = r0 + (zk % A.nzr) * A.zc;
+    K.z1 = min(K.z0 + A.zc, r0 + A.zlen);
+    K.plane = (size_t)Lx * (size_t)Ly;
+    K.pbytes = (uint32_t)(K.plane * sizeof(float));
+    K.qplane = (uint32_t)(K.plane >> 2);
+    if constexpr (WH) {
+        const int nbytes = (int)((uint32_t)(A.nz + 2 * A.gz) * K.pbytes);
+        K.rin = __builtin_amdgcn_make_buffer_rsrc((void *)A.in, (short)0, nbytes, 0x00020000);
+        K.rout = __builtin_amdgcn_make_buffer_rsrc((void *)A.out, (short)0, nbytes, 0x00020000);
+    }
+    K.qwrap = (uint32_t)A.Lzg * K.qplane;
+    K.m2v = f32x2{A.m2, A.m2};
+    asm volatile("" : "+v"(K.m2v));
+    // periodic: plane k+3 = nz is local plane 0 again; slabs never wrap
+    K.swrap_at = A.periodic ? A.nz : INT_MIN;
+    const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
+    K.slo = (uint32_t)s0;
+    K.shi = (uint32_t)(s0 >> 32);
+    K.slo1 = (uint32_t)s1;
+    K.shi1 = (uint32_t)(s1 >> 32);
+    const int xl = (x0 == 0 ? Lx : x0) - 1, xr = x0 + 256 == Lx ? 0 : x0 + 256;
+    auto wrapy = [Ly](int y) { return y < 0 ? y + Ly : (y >= Ly ? y - Ly : y); };
+    const bool xw = WIDE && K.w == kTbWaves;
+    // waves 0 and kTbWaves-1 also carry the rows beyond the band (y0-2, y0+9) into in_lds
+    const bool xrow = K.w == 0 || K.w == kTbWaves - 1;
+    const int xslot = K.w == 0 ? 0 : kTpRows - 1;
+    uint32_t vxr = kTpOob;  // waves 1..8 carry no row beyond the band: their X loads are dropped
+    if (!xw) {
+        const int y = wrapy(yb * kTbRows - 1 + K.w);
+        const int yx = wrapy(K.w == 0 ? y - 1 : y + 1);
+        K.voff = (uint32_t)((y * Lx + x0 + 4 * K.lane) * 4);
+        if (xrow) vxr = (uint32_t)((yx * Lx + x0 + 4 * K.lane) * 4);
+        K.vm = K.vp = 0;
+        K.vex = (uint32_t)((y * Lx + (K.lane == 63 ? xr : xl)) * 4);
+        K.vx2 = 0;
+        K.qoff = (uint32_t)((y * Lx + x0 + 4 * K.lane) >> 2);
+    } else {  // x-halo wave lanes 0..7: (x0-1, y0+l); 8..15: (x0+256, y0+l-8); the rest repeat lane 0
+        const int l = K.lane < 16 ? K.lane : 0;
+        const int y = wrapy(yb * kTbRows + (l & 7)), ym = wrapy(y - 1), yp = wrapy(y + 1);
+        const int xe = (l >> 3) ? xr : xl;
+        const int xem = xe == 0 ? Lx - 1 : xe - 1, xep = xe == Lx - 1 ? 0 : xe + 1;
+        K.voff = (uint32_t)((y * Lx + xe) * 4);
+        K.vex = (uint32_t)((y * Lx + xem) * 4);
+        K.vx2 = (uint32_t)((y * Lx + xep) * 4);
+        K.vm = (uint32_t)((ym * Lx + xe) * 4);
+        K.vp = (uint32_t)((yp * Lx + xe) * 4);
+        K.qoff = (uint32_t)((y * Lx + xe) >> 2);
+    }
+    __shared__ float4 in_lds[2][kTpRows][64];
+    __shared__ float4 t_lds[2][kTbWaves][64];
+    __shared__ float tx[WIDE ? 2 : 1][kTbWaves][2];
+
+    // prologue: planes z0-2, z0-1, z0 (own rows), the rows beyond of z0-1 and
+    // z0, edge sites / x-halo neighbours of plane z0-1; plane z0-1 published
+    const __amdgpu_buffer_rsrc_t p0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
+    const __amdgpu_buffer_rsrc_t p1 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 1), K.plane, K.pbytes);
+    const __amdgpu_buffer_rsrc_t p2 = plane_rsrc(A.in, tb_pidx(A, K.z0), K.plane, K.pbytes);
+    __shared__ float bmx[2];
+    if constexpr (FR) {
+        if (threadIdx.x < 2) bmx[threadIdx.x] = -__builtin_inff();
+    }
+    FrameAcc f1 = frame_acc(), f2 = frame_acc();
+    TpRun R;
+    R.s1 = (uint32_t)tb_pidx(A, K.z0) * K.pbytes;
+    R.s2 = (uint32_t)tb_pidx(A, K.z0 + 1) * K.pbytes;
+    R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
+    R.qzm = 0;
+    const int z1 = K.z1;
+    // the two roles march in loops of their own (one barrier per iteration in
+    // each, the same iteration count), so their registers do not add up
+    if (!xw) {
+        float4 I[4], T[4], X[2];
+        float E[2] = {0.f, 0.f};
+        I[0] = bload4(p0, K.voff);
+        I[1] = bload4(p1, K.voff);
+        I[2] = bload4(p2, K.voff);
+        X[0] = bload4(p1, vxr);
+        X[1] = bload4(p2, vxr);
+        if constexpr (WIDE) E[0] = bload1(p1, K.vex);
+        in_lds[0][K.w + 1][K.lane] = I[1];
+        if (xrow) in_lds[0][xslot][K.lane] = X[0];
+        T[0] = T[1] = T[2] = T[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+        for (int k = K.z0 - 1; k <= z1; k += 4) {
+            tp_row<NZ, WIDE, FR, WH, 0>(A, K, R, k, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
+            if (k + 1 > z1) break;
+            tp_row<NZ, WIDE, FR, WH, 1>(A, K, R, k + 1, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
+            if (k + 2 > z1) break;
+            tp_row<NZ, WIDE, FR, WH, 2>(A, K, R, k + 2, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
+            if (k + 3 > z1) break;
+            tp_row<NZ, WIDE, FR, WH, 3>(A, K, R, k + 3, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
+        }
+    } else {
+        float C[4];
+        float4 NB[2];
+        C[0] = bload1(p0, K.voff);
+        C[1] = bload1(p1, K.voff);
+        C[2] = bload1(p2, K.voff);
+        NB[0] = make_float4(bload1(p1, K.vex), bload1(p1, K.vx2), bload1(p1, K.vm), bload1(p1, K.vp));
+        __syncthreads();
+        for (int k = K.z0 - 1; k <= z1; k += 4) {
+            tp_xhalo<NZ, WH, 0>(A, K, R, k, C, NB, tx);
+            if (k + 1 > z1) break;
+            tp_xhalo<NZ, WH, 1>(A, K, R, k + 1, C, NB, tx);
+            if (k + 2 > z1) break;
+            tp_xhalo<NZ, WH, 2>(A, K, R, k + 2, C, NB, tx);
+            if (k + 3 > z1) break;
+            tp_xhalo<NZ, WH, 3>(A, K, R, k + 3, C, NB, tx);
+        }
+    }
+    if constexpr (FR) {
         __shared__ uint64_t sk[kTbWaves + 1];
         __shared__ uint32_t sa[kTbWaves + 1];
         frame_flush(A, f1, 0, sk, sa);
@@ -1147,8 +1446,12 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     const void *fn;
     // one 32-bit (signed, < 2^31 B) descriptor per padded buffer when it fits
     const bool wh = (long long)(a.nz + 2 * a.gz) * a.Lx * a.Ly * 4 < (1ll << 31);
-#define SQ_TB2F(N, W, E, F) (wh ? (const void *)&phi4_tb2_kernel<N, W, E, F, true> \
-                             : (const void *)&phi4_tb2_kernel<N, W, E, F, false>)
+    // SQ_TB2_PIPE=0: the round-2 kernel (loads consumed in the iteration that issues them)
+    const char *pe = getenv("SQ_TB2_PIPE");  // read per launch (tests switch it within a process)
+    const bool pipe = pe ? atoi(pe) != 0 : true;
+#define SQ_TB2K(N, W, E, F, H) (pipe ? (const void *)&phi4_tb2p_kernel<N, W, E, F, H> \
+                                     : (const void *)&phi4_tb2_kernel<N, W, E, F, H>)
+#define SQ_TB2F(N, W, E, F) (wh ? SQ_TB2K(N, W, E, F, true) : SQ_TB2K(N, W, E, F, false))
 #define SQ_TB2(N, W, E) (fr ? SQ_TB2F(N, W, E, true) : SQ_TB2F(N, W, E, false))
     if (wide && wpe == 6)
         fn = nz ? SQ_TB2(true, true, 6) : SQ_TB2(false, true, 6);
@@ -1158,6 +1461,7 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
         fn = nz ? SQ_TB2(true, false, 1) : SQ_TB2(false, false, 1);
 #undef SQ_TB2
 #undef SQ_TB2F
+#undef SQ_TB2K
     Phi4StepArgs q = a;
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);

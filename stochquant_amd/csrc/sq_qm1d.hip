@@ -46,6 +46,11 @@ __device__ __forceinline__ double ddpot(double x, int pot) {  // ddPot(), :190-1
     return 2.;
 }
 __device__ __forceinline__ double absol(double v) { return v <= 0 ? -v : v; }
+// potID 3: the float tanhf inside clas() (x_cl = kEta * (double) of it)
+__device__ __forceinline__ float xcl_tanh(double t, double w) {
+    const double s = 2.0;  // (double)sqrtf((float)(2.*V0/m)) == 2 exactly
+    return sq_glibc_tanhf((float)(s * (t - w) / kEta));
+}
 
 __device__ __forceinline__ double wave_incl_max(double v, int lane) {
 #pragma unroll
@@ -66,7 +71,10 @@ __device__ __forceinline__ double pick(const double (&v)[K], int k) {  // v[k], 
 }
 
 // One frame, N <= 4,096: thread g (= 64 wave + lane) owns sites [gK, gK+K)
-// in registers; W = blockDim/64 <= 16 waves (MW) or one wave.  Per step:
+// in registers; W = blockDim/64 <= 16 waves (MW) or one wave.  The
+// field-independent work -- omega's recurrence, the site normals, potID 3's
+// x_cl and ddPot -- comes precomputed from qm1d_prep_launch's tables (read one
+// step ahead), so a step is only the chain's own arithmetic.  Per step:
 //   1. site updates from the old field (left/right neighbours by DPP wave
 //      shifts; across waves through LDS), running means, guard, X', drift
 //      check;
@@ -76,11 +84,36 @@ __device__ __forceinline__ double pick(const double (&v)[K], int k) {  // v[k], 
 //      exceeds X'(E) (leaders are strict running-maximum records), V' =
 //      max(V, max |X'|), a site is an unstable leader iff X' exceeds every X'
 //      before it and X'(E) while its drift check exceeds V and every |X'|
-//      before it (oracle/orc_qm1d.c orc_qm1d_frame, tau_kernel.cl:135-143);
-//   3. omega from its counter-based normal (drawn 64 steps at a time, one
-//      step per lane, and read back with readlane).
+//      before it (oracle/orc_qm1d.c orc_qm1d_frame, tau_kernel.cl:135-143).
 // One wave needs no barrier at all (readlane / ballot); W waves use two per
 // step, with the LDS slots double-buffered by step parity.
+template <int K>
+struct StepTab {  // one step's table values of a lane's K sites
+    float xi[K], t[K];
+    double dd[K];
+    float tl, tr, tm;  // x_cl tanhf at -a, N a and mid a (potID 3)
+};
+
+template <int K>
+__device__ __forceinline__ void load_tab(const Qm1dArgs &A, int j, int i0, int mid, bool p3, StepTab<K> &T) {
+    const int N = A.N, nq4 = (N + 3) & ~3;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int i = min(i0 + k, N - 1);
+        T.xi[k] = A.xi[(size_t)j * nq4 + i];
+        if (p3) {
+            T.t[k] = A.tcl[(size_t)j * (N + 2) + i + 1];
+            T.dd[k] = A.dd[(size_t)j * N + i];
+        }
+    }
+    if (p3) {
+        const float *r = A.tcl + (size_t)j * (N + 2);
+        T.tl = r[0];
+        T.tr = r[N + 1];
+        T.tm = r[mid + 1];
+    }
+}
+
 template <int K, bool MW>
 __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs A) {
     constexpr int kW = 16;
@@ -89,10 +122,11 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
     __shared__ double s_fmid[2], s_xe[2];
 
     const int N = A.N, pot = A.pot, mid = N / 2;
+    const bool p3 = pot == 3;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int W = MW ? (int)(blockDim.x >> 6) : 1;
     const int i0 = (int)threadIdx.x * K;
-    const double h = A.h, a = A.a, a2 = A.a2;
+    const double h = A.h, a2 = A.a2;
     const double ninf = -__builtin_inf();
 
     double f[K], x[K], xx0[K], Xn[K], dchk[K];
@@ -103,7 +137,6 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
         x[k] = i < N ? A.x[i] : 0.;
         xx0[k] = i < N ? A.xx0[i] : 0.;
     }
-    double om = A.st->omega_in;
     int E = A.st->lrgEl;
     double V = A.st->lrgVl;
     int stable = 1, steps = 0;
@@ -121,34 +154,14 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
     } else {
         fmid = readlane_d(pick(f, mid % K), mid / K);
     }
-    float wnoise = 0.f;  // omega's normals for 64 steps, one step per lane
+    StepTab<K> cur, nxt;
+    load_tab<K>(A, 0, i0, mid, p3, cur);
 
     for (int j = 0; j < A.loops; ++j) {
         const int p = j & 1;
-        const unsigned long long step = A.tick + (unsigned long long)j;
-        const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-        if ((j & 63) == 0) {
-            const unsigned long long sl = step + (unsigned long long)lane;
-            wnoise = normals4(0ull, kStreamOmega, (uint32_t)sl, (uint32_t)(sl >> 32), A.k0, A.k1).a;
-        }
+        if (j + 1 < A.loops) load_tab<K>(A, j + 1, i0, mid, p3, nxt);  // one step ahead
         // ---- 1. site updates ----
-        float nz[K < 4 ? 4 : K];
-        if constexpr (K >= 4) {
-#pragma unroll
-            for (int q = 0; q < K / 4; ++q) {
-                const f32x4n n = normals4((unsigned long long)((i0 >> 2) + q), kStreamField, slo, shi, A.k0, A.k1);
-                nz[4 * q] = n.a;
-                nz[4 * q + 1] = n.b;
-                nz[4 * q + 2] = n.c;
-                nz[4 * q + 3] = n.d;
-            }
-        } else {
-            const f32x4n n = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
-            const float q4[4] = {n.a, n.b, n.c, n.d};
-#pragma unroll
-            for (int k = 0; k < K; ++k) nz[k] = q4[(i0 & 3) + k];
-        }
-        const double Xm = fmid + xcl((double)mid * a, om, pot);
+        const double Xm = fmid + (p3 ? kEta * (double)cur.tm : 0.);
         const double den = (double)(A.runs + j + 1);
         double prev_old = fL;  // old f[i-1]
         double lmaxX = ninf, lmaxA = ninf;
@@ -160,18 +173,19 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
             dchk[k] = 0.;
             if (i < N) {
                 const double fi = f[k];
-                const double xc = xcl((double)i * a, om, pot);
-                const double dw = A.sig * (double)nz[k];
+                const double xc = p3 ? kEta * (double)cur.t[k] : 0.;  // clas(), :184-189
+                const double dp = p3 ? cur.dd[k] : 2.;                // ddPot(), :190-195
+                const double dw = A.sig * (double)cur.xi[k];
                 const double fr = (k + 1 < K) ? f[k + 1] : fR;
                 double v;
                 if (i == 0)
-                    v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
-                        ddpot(xc, pot) * fi * h + dw;
+                    v = fi + kM * h * (fr + (-kEta) - (p3 ? kEta * (double)cur.tl : 0.) - 2 * fi) / a2 -
+                        dp * fi * h + dw;
                 else if (i == N - 1)
-                    v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
-                        ddpot(xc, pot) * fi * h + dw;
+                    v = fi + kM * h * (prev_old + kEta - (p3 ? kEta * (double)cur.tr : 0.) - 2 * fi) / a2 -
+                        dp * fi * h + dw;
                 else
-                    v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
+                    v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - dp * fi * h + dw;
                 if (v > 1000) v = 1000;  // guard, :119-133
                 if (v < -1000) v = -1000;
                 if (v != v) v = 1000;
@@ -261,18 +275,12 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
         }
         if (gX > XE) E = garg;
         V = totA;
-        // ---- 3. collective coordinate, :103-110,155-167 (uniform) ----
-        const float xw = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wnoise), j & 63));
-        const double nwo = om + A.kconst * (A.sigw * (double)xw);
-        const double top = (double)(N - 1) * a;
-        if (nwo > top) om = 2 * (double)(N - 1) * a - nwo;
-        else if (nwo < 0) om = -nwo;
-        else om = nwo;
         steps = j + 1;
         if (any) {
             stable = 0;
             break;
         }
+        cur = nxt;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -284,11 +292,68 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
         }
     }
     if (threadIdx.x == 0) {
-        A.st->omega_out = om;
+        A.st->omega_out = A.om[steps];  // the collective coordinate after the last step run
         A.st->lrgEl = E;
         A.st->lrgVl = V;
         A.st->stable = stable;
         A.st->steps_done = steps;
+    }
+}
+
+// omega at the start of every step of a frame, om[0..loops] (item N's scalar
+// recurrence, tau_kernel.cl:103-110,155-167), one wave: the normals of 64
+// steps at once, one step per lane, the recurrence by readlane.
+__global__ __launch_bounds__(64) void qm1d_omega_kernel(const Qm1dArgs A) {
+    const int lane = threadIdx.x;
+    const int N = A.N;
+    double om = A.st->omega_in;
+    if (lane == 0) A.om[0] = om;
+    const double top = (double)(N - 1) * A.a;
+    for (int j0 = 0; j0 < A.loops; j0 += 64) {
+        const unsigned long long sl = A.tick + (unsigned long long)(j0 + lane);
+        const float w = normals4(0ull, kStreamOmega, (uint32_t)sl, (uint32_t)(sl >> 32), A.k0, A.k1).a;
+        const double d = A.kconst * (A.sigw * (double)w);
+        const int n = min(64, A.loops - j0);
+        for (int q = 0; q < n; ++q) {
+            const double nwo = om + readlane_d(d, q);
+            if (nwo > top) om = 2 * (double)(N - 1) * A.a - nwo;
+            else if (nwo < 0) om = -nwo;
+            else om = nwo;
+            if (lane == 0) A.om[j0 + q + 1] = om;
+        }
+    }
+}
+
+// The site normals of every step (4 per Philox call, quad q of step j) and,
+// potID 3, x_cl's tanhf at i = -1..N and ddPot at i = 0..N-1 for omega om[j].
+__global__ __launch_bounds__(256) void qm1d_tables_kernel(const Qm1dArgs A) {
+    const int N = A.N, nq = (N + 3) >> 2, nq4 = nq * 4;
+    const long long total = (long long)A.loops * nq;
+    for (long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+         g += (long long)gridDim.x * blockDim.x) {
+        const int j = (int)(g / nq), q = (int)(g % nq);
+        const unsigned long long step = A.tick + (unsigned long long)j;
+        const f32x4n n = normals4((unsigned long long)q, kStreamField, (uint32_t)step, (uint32_t)(step >> 32), A.k0,
+                                  A.k1);
+        float *xo = A.xi + (size_t)j * nq4 + 4 * q;
+        xo[0] = n.a;
+        xo[1] = n.b;
+        xo[2] = n.c;
+        xo[3] = n.d;
+        if (A.pot == 3) {
+            const double w = A.om[j];
+            float *to = A.tcl + (size_t)j * (N + 2);
+            double *dout = A.dd + (size_t)j * N;
+            for (int i = 4 * q; i < min(4 * q + 4, N); ++i) {
+                const float t = xcl_tanh((double)i * A.a, w);
+                to[i + 1] = t;
+                dout[i] = ddpot(kEta * (double)t, 3);
+            }
+            if (q == 0) {
+                to[0] = xcl_tanh(-1. * A.a, w);
+                to[N + 1] = xcl_tanh((double)N * A.a, w);
+            }
+        }
     }
 }
 
@@ -471,6 +536,14 @@ template <int K>
 static void launch_wave(const Qm1dArgs &a, int W, hipStream_t s) {
     if (W == 1) hipLaunchKernelGGL((qm1d_frame_wave<K, false>), dim3(1), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((qm1d_frame_wave<K, true>), dim3(1), dim3(64 * W), 0, s, a);
+}
+
+hipError_t qm1d_prep_launch(const Qm1dArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL(qm1d_omega_kernel, dim3(1), dim3(64), 0, s, a);
+    const long long total = (long long)a.loops * ((a.N + 3) / 4);
+    const unsigned grid = (unsigned)std::max(1ll, std::min(2048ll, (total + 255) / 256));
+    hipLaunchKernelGGL(qm1d_tables_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {

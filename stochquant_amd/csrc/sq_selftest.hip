@@ -6,6 +6,7 @@
 #include <algorithm>
 
 #include "sq_glibcf.h"
+#include "sq_dpp.h"
 #include "sq_internal.h"
 #include "sq_rng.h"
 
@@ -86,12 +87,74 @@ __global__ __launch_bounds__(256) void copy_kernel(const f4v *__restrict__ in, f
 
 }  // namespace
 
+// DPP cross-wave stress (the round-3 frame-record finding): the
+// waves of a 16-wave block either run the frame records' wave-max scan
+// (row_shr 1/2/4/8 + row_bcast 15/31 with row masks, sq_dpp.h dpp_all_max_f)
+// or the stencil's x-neighbour rotation (wave_ror:1 / wave_rol:1 DPP fused into
+// an add), checking every rotated value against the exact lane-1 / lane+1
+// value; errs[lane] counts the lanes that got a wrong one.  mode 0: every wave
+// rotates (control); 1: even waves scan, odd waves rotate; 2: every wave scans
+// and rotates in turn; 3: as 1 with the scan's row_bcast steps left out.
+__device__ __forceinline__ float mix_val(int lane, int wave, int it) {
+    return (float)((lane * 131 + wave * 17 + it * 7) & 1023) * 0.25f + 1.0f;
+}
+template <int M>
+__device__ __forceinline__ float mix_scan(float v) {
+    const float id = -__builtin_inff();
+    v = fmaxf(v, dpp_f<0x111, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x112, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x114, 0xf, 0xf>(v, id));
+    v = fmaxf(v, dpp_f<0x118, 0xf, 0xf>(v, id));
+    if constexpr (M != 3) {
+        v = fmaxf(v, dpp_f<0x142, 0xa, 0xf>(v, id));
+        v = fmaxf(v, dpp_f<0x143, 0xc, 0xf>(v, id));
+    }
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+template <int M>
+__global__ __launch_bounds__(1024) void dpp_mix_kernel(int iters, unsigned *errs, float *sink) {
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const bool scanner = (M == 1 || M == 3) ? (wave & 1) == 0 : M == 2;
+    const bool rotator = M == 0 || M == 2 || (wave & 1) == 1;
+    float acc = 0.f;
+    unsigned bad = 0;
+    for (int it = 0; it < iters; ++it) {
+        const float v = mix_val(lane, wave, it), w = mix_val(lane, wave, it + 1);
+        if (scanner) {
+            // the records' shape: a ballot, a divergent per-lane update, the scan
+            if (__ballot(v > 200.f) != 0ull) {
+                if (v > acc) acc = v;
+                acc = fmaxf(acc, mix_scan<M>(acc + v));
+            }
+        }
+        if (rotator) {
+            const float l = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x13C, 0xF, 0xF, true));
+            const float r = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x134, 0xF, 0xF, true));
+            const float sl = l + w, sr = r + w;  // fused into v_add_f32_dpp like the stencil's x-sums
+            const float el = mix_val((lane + 63) & 63, wave, it) + w, er = mix_val((lane + 1) & 63, wave, it) + w;
+            bad += (sl != el) + (sr != er);
+        }
+    }
+    if (bad) atomicAdd(errs + lane, bad);
+    if (acc == 12345.f) sink[threadIdx.x] = acc;  // keeps the scans alive
+}
+
 hipError_t selftest_normals_launch(float *out, size_t nquads, unsigned long long quad0,
                                    uint32_t stream, unsigned long long step, uint32_t k0,
                                    uint32_t k1, hipStream_t s) {
     const unsigned grid = (unsigned)((nquads + 255) / 256);
     hipLaunchKernelGGL(normals_kernel, dim3(grid), dim3(256), 0, s, out, nquads, quad0, stream, step,
                        k0, k1);
+    return hipGetLastError();
+}
+
+hipError_t selftest_dpp_mix_launch(int mode, int blocks, int iters, unsigned *errs, float *sink, hipStream_t s) {
+    switch (mode) {
+    case 0: hipLaunchKernelGGL(dpp_mix_kernel<0>, dim3(blocks), dim3(1024), 0, s, iters, errs, sink); break;
+    case 1: hipLaunchKernelGGL(dpp_mix_kernel<1>, dim3(blocks), dim3(1024), 0, s, iters, errs, sink); break;
+    case 2: hipLaunchKernelGGL(dpp_mix_kernel<2>, dim3(blocks), dim3(1024), 0, s, iters, errs, sink); break;
+    default: hipLaunchKernelGGL(dpp_mix_kernel<3>, dim3(blocks), dim3(1024), 0, s, iters, errs, sink); break;
+    }
     return hipGetLastError();
 }
 

@@ -51,3 +51,16 @@ def rank_main(conn, rank, nranks, shape, kw, env, script):
         if lat is not None:
             lat.close()
         conn.close()
+
+
+def run_cmd(conn, argv, env, timeout):
+    """Run a command from the fork server (a process that never touched the GPU)
+    and send back (returncode, stdout, stderr)."""
+    import subprocess
+    try:
+        r = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, env=env)
+        conn.send((r.returncode, r.stdout, r.stderr))
+    except Exception:
+        conn.send((-1, "", traceback.format_exc()))
+    finally:
+        conn.close()

@@ -188,3 +188,44 @@ def test_p2p_frames_with_noise(gpu):
         assert o["stable"] == mono["stable"] == [True, True]
         assert o["TV"] == mono["TV"]
     assert np.array_equal(_assemble(outs), mono["field"][0])
+
+
+def _bench(args, timeout=240):
+    """bench.py in a child of the fork server; returns its JSON line."""
+    import json
+    import os
+    import sys
+    from conftest import ROOT
+    from p2p_ranks import run_cmd
+    ctx = rank_context()
+    a, b = ctx.Pipe()
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = ctx.Process(target=run_cmd, args=(b, [sys.executable, os.path.join(ROOT, "bench.py")] + args, env,
+                                          timeout), daemon=True)
+    p.start()
+    b.close()
+    assert a.poll(timeout + 30), "bench.py did not finish"
+    rc, out, err = a.recv()
+    p.join(10)
+    assert rc == 0, err[-3000:]
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_bench_multi_rank_check(gpu, corrupt):
+    """bench.py's self-check of a multi-rank run (stochquant_amd/verify.py): two
+    P2P rank processes of the bench's own spawn -> gloo -> connect path on one
+    GPU run the check protocol and compare each slab's digest with the golden
+    single-GPU run of the 256 x 256 x 512 lattice: "pass"; with one value of
+    rank 1's slab flipped: "fail"."""
+    args = ["--gpus", "2", "--comm", "p2p", "--same-device", "--steps", "4", "--warmup", "2",
+            "--settle-ms", "0", "--no-cpu-baseline", "--no-c3"]
+    if corrupt:
+        args += ["--corrupt-rank", "1"]
+    d = _bench(args)
+    assert d["n_gpus"] == 2 and d["config"]["lattice"] == [256, 256, 512]
+    assert d["multi_rank_check"] == ("fail" if corrupt else "pass")

@@ -807,3 +807,30 @@ def test_stable_frames_equal_raw_steps(gpu, oracle_mod, monkeypatch, path):
             return L.download()
 
     assert np.array_equal(run(True), run(False))
+
+
+@pytest.mark.parametrize("pipe", ["1", "0"])
+@pytest.mark.parametrize("shape", [(256, 8, 16), (256, 16, 24)])
+def test_frame_launches_equal_raw_steps_repeated(gpu, oracle_mod, monkeypatch, pipe, shape):
+    """A frame of 4 steps equals 4 raw steps, repeated: the test that catches
+    round 2's one-accumulator frame variant (a 16-byte store whose first data
+    register a VALU overwrote at once: lanes 12-15 of every 16 of one output row
+    stored the new value, in most runs; stochquant_amd/isa_check.py).  Both
+    fused kernels (SQ_TB2_PIPE=1 pipelined, 0 round 2's)."""
+    monkeypatch.setenv("SQ_TB2_PIPE", pipe)
+    rng = np.random.default_rng(77)
+    phi0 = (0.9 * rng.standard_normal((shape[2], shape[1], shape[0]))).astype(np.float32)
+
+    def run(frames):
+        with _lat(shape, loops=4, dtau=0.02, m2=0.5, lam=1.0, seed=77) as L:
+            L.upload(phi0)
+            L.step(1)
+            if frames:
+                assert L.run_frame()
+            else:
+                L.step(4)
+            return L.download()
+
+    ref = run(False)
+    for _ in range(8):
+        assert np.array_equal(run(True), ref)
