@@ -153,6 +153,14 @@ int sq_qm1d_noise_consumed(sq_ctx *ctx, unsigned long long *n);
  * failure :533-554 (kept on device, no host round trip), and, if
  * adapt_dtau, the reference Δτ controller :523-541. */
 int sq_run_frame(sq_ctx *ctx, int *stable);
+/* nframes frames back to back, as nframes sq_run_frame calls (same field,
+ * verdicts, Δτ sequence, stability state and last-frame records, bit for
+ * bit): stable[f] is frame f's verdict, dtau[f] (nullable) the Δτ after it
+ * (what the next frame runs at).  PHI4, one slab without an exchange: the
+ * verdict, rollback and Δτ controller run on the device between frames (no
+ * host round trip; one read-back per call).  Replaces a caller's loop over
+ * tauhost.c:479-560 when no per-frame observable is needed in between. */
+int sq_run_frames(sq_ctx *ctx, int nframes, int *stable, double *dtau);
 
 /* PHI4: raw Langevin steps without frame control (the bench's hot path). */
 int sq_step(sq_ctx *ctx, int nsteps);

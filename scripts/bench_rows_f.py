@@ -43,9 +43,19 @@ def main():
         lat.sync()
         raw = timed(lambda: lat.step(a.loops), a.reps, lat.sync)
         frame = timed(lambda: lat.run_frame(), a.reps, lat.sync)
+        batch = timed(lambda: lat.run_frames(a.reps), 3, lat.sync) / a.reps
+        os.environ["SQ_FRAME_HOST"] = "1"
+        host = timed(lambda: lat.run_frame(), a.reps, lat.sync)
+        del os.environ["SQ_FRAME_HOST"]
         print(json.dumps({"row": "f1 frame control", "loops": a.loops, "raw_steps_us": round(raw * 1e6, 1),
                           "frame_us": round(frame * 1e6, 1), "overhead_us_per_frame": round((frame - raw) * 1e6, 1),
-                          "overhead_frac": round(frame / raw - 1, 4)}), flush=True)
+                          "overhead_frac": round(frame / raw - 1, 4),
+                          "batch_frame_us": round(batch * 1e6, 1),
+                          "batch_overhead_us_per_frame": round((batch - raw) * 1e6, 1),
+                          "batch_overhead_frac": round(batch / raw - 1, 4),
+                          "host_decided_frame_us": round(host * 1e6, 1),
+                          "note": "frame: sq_run_frame (device controller, one sync per frame); batch: "
+                                  "sq_run_frames(reps) per frame; host_decided: SQ_FRAME_HOST=1"}), flush=True)
         mom = timed(lambda: lat.moments(), a.reps, lat.sync)
         cor = timed(lambda: lat.correlator(), a.reps, lat.sync)
         print(json.dumps({"row": "f2 observables", "moments_us": round(mom * 1e6, 1),

@@ -99,6 +99,7 @@ SIGNATURES = {
     "sq_qm1d_get_scan": (ctypes.c_int, [_P, _I, _D, ctypes.POINTER(ctypes.c_ulonglong)]),
     "sq_qm1d_set_scan": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_double, ctypes.c_ulonglong]),
     "sq_run_frame": (ctypes.c_int, [_P, _I]),
+    "sq_run_frames": (ctypes.c_int, [_P, ctypes.c_int, _I, _D]),
     "sq_step": (ctypes.c_int, [_P, ctypes.c_int]),
     "sq_upload_field": (ctypes.c_int, [_P, _F, ctypes.c_size_t]),
     "sq_download_field": (ctypes.c_int, [_P, _F, ctypes.c_size_t]),

@@ -201,6 +201,15 @@ struct sq_ctx {
     float stab_T = 0, stab_V = 0;        // carried across frames, never rolled back (as lrgEl / lrgVl)
     int stab_fired = -1;                 // step of the last frame at which the rule fired, -1 none
     std::vector<float> rec_M, rec_D, rec_A;  // the last frame's per-step records
+    // device frame control (phi4_frames_dev): controller state and its pinned
+    // mirror, the last frame's folded records (M | D | A, loops floats each) and
+    // per-frame verdicts / Δτ of a batch (fr_cap entries, device and pinned)
+    sq::FrameCtl *ctl = nullptr, *ctl_host = nullptr;
+    float *rec_dev = nullptr;
+    int *fr_stable = nullptr, *fr_stable_h = nullptr;
+    double *fr_dtau = nullptr, *fr_dtau_h = nullptr;
+    int fr_cap = 0;
+    bool dev_frames = false;  // the current frame's launches read {h, sig, sigq} from ctl->coef
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
@@ -348,6 +357,7 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.flag = c->in_frame ? c->flag : nullptr;  // the guard flag only feeds a frame's rollback
     a.st_md = nullptr;
     a.st_a = nullptr;
+    a.dcoef = (c->in_frame && c->dev_frames) ? c->ctl->coef : nullptr;
     if (c->in_frame && c->st_md != nullptr) {
         const size_t k = (size_t)(c->step - c->frame_step0) * sq::kStabSlots;
         a.st_md = c->st_md + k;
@@ -1424,6 +1434,114 @@ int phi4_frame(sq_ctx *c, int *stable) {
     return SQ_OK;
 }
 
+// Frames back to back under the device controller: per frame
+// the launches of phi4_frame (snapshot from the first fused launch, the frame
+// instances with the guard flag and the records), then phi4_frame_ctl_kernel
+// (record fold, stab_rule, Δτ) and phi4_rollback_kernel (a no-op when
+// stable); the launches of frame f+1 read the coefficients frame f's
+// controller wrote.  One read-back at the end of the batch.  Bit-identical to
+// the host path (phi4_frame + adapt) in field, verdicts, Δτ, T/V and records.
+// One slab without an exchange; other decompositions (and loops < 1, a field
+// not yet through the guard, SQ_FRAME_HOST=1) take the host path per frame.
+int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
+    const int L = c->p.loops;
+    const bool one_stream = c->slabs.size() == 1 && c->p.comm == SQ_COMM_NONE;
+    const char *fh = getenv("SQ_FRAME_HOST");
+    const bool host_only = !one_stream || L < 1 || c->st_md == nullptr || (fh && atoi(fh) != 0);
+    int f = 0;
+    while (f < n && (host_only || !c->field_finite)) {  // host path (rollback restores fin0 = false)
+        int rc = phi4_frame(c, &stable[f]);
+        if (rc) return rc;
+        adapt(c, stable[f]);
+        if (dtau_out) dtau_out[f] = c->dtau;
+        ++f;
+    }
+    if (f == n) return SQ_OK;
+    Slab &s0 = c->slabs[0];
+    const hipStream_t st = s0.sA;
+    const size_t plane = plane_floats(c), nfl = (size_t)s0.nz * plane;
+    if (!c->stab_init) {
+        int rc = phi4_field_max(c, &c->stab_T, &c->stab_V);
+        if (rc) return rc;
+        c->stab_init = true;
+    }
+    if (!c->ctl) {
+        SQ_HIP(hipMalloc(&c->ctl, sizeof(sq::FrameCtl)));
+        SQ_HIP(hipHostMalloc(&c->ctl_host, sizeof(sq::FrameCtl), hipHostMallocDefault));
+        SQ_HIP(hipMalloc(&c->rec_dev, 3 * sizeof(float) * (size_t)L));
+    }
+    if (!s0.snap) SQ_HIP(hipMalloc(&s0.snap, nfl * sizeof(float)));
+    const int m = n - f;
+    if (m > c->fr_cap) {
+        (void)hipFree(c->fr_stable);
+        (void)hipFree(c->fr_dtau);
+        if (c->fr_stable_h) (void)hipHostFree(c->fr_stable_h);
+        if (c->fr_dtau_h) (void)hipHostFree(c->fr_dtau_h);
+        c->fr_cap = 0;
+        SQ_HIP(hipMalloc(&c->fr_stable, sizeof(int) * (size_t)m));
+        SQ_HIP(hipMalloc(&c->fr_dtau, sizeof(double) * (size_t)m));
+        SQ_HIP(hipHostMalloc(&c->fr_stable_h, sizeof(int) * (size_t)m, hipHostMallocDefault));
+        SQ_HIP(hipHostMalloc(&c->fr_dtau_h, sizeof(double) * (size_t)m, hipHostMallocDefault));
+        c->fr_cap = m;
+    }
+    // the controller starts from the host's state (a caller may have set Δτ or T/V)
+    sq::FrameCtl &h = *c->ctl_host;
+    memset(&h, 0, sizeof h);
+    h.dtau = c->dtau;
+    h.C = c->p.C;
+    const float hf = (float)c->dtau;  // as phi4_base_args
+    h.coef[0] = hf;
+    h.coef[1] = (float)(sqrt(2.0 * (double)hf) * c->p.C);
+    h.coef[2] = (float)(sqrt(2.0 * (double)hf) * c->p.C * sq::kSqrt2Ln2);
+    h.T = c->stab_T;
+    h.V = c->stab_V;
+    h.stab_cnt = c->stab_cnt;
+    h.adapt = c->p.adapt_dtau ? 1 : 0;
+    h.stable = 1;
+    h.fired = -1;
+    SQ_HIP(hipMemcpyAsync(c->ctl, c->ctl_host, sizeof h, hipMemcpyHostToDevice, st));
+    if (!c->frame_rec_zero) SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, st));
+    c->frame_rec_zero = true;  // every controller launch leaves the records and the flag zero
+    const bool snap_in_kernel = c->tbz > 0 && L >= 2;
+    for (int i = 0; i < m; ++i) {
+        if (snap_in_kernel)
+            c->snap_next = s0.snap;
+        else
+            SQ_HIP(hipMemcpyAsync(s0.snap, plane0(c, s0, c->cur), nfl * sizeof(float), hipMemcpyDeviceToDevice, st));
+        c->in_frame = true;
+        c->dev_frames = true;
+        c->frame_step0 = c->step;
+        int rc = phi4_steps(c, L);
+        c->in_frame = false;
+        c->dev_frames = false;
+        c->snap_next = nullptr;
+        if (rc) return rc;
+        SQ_HIP(sq::phi4_frame_ctl_launch(c->ctl, c->st_md, c->st_a, c->flag, L, c->rec_dev, c->fr_stable + i,
+                                         c->fr_dtau + i, st));
+        SQ_HIP(sq::phi4_rollback_launch(c->ctl, plane0(c, s0, c->cur), s0.snap, nfl, st));
+        c->perf.kernel_launches += 2;
+    }
+    SQ_HIP(hipMemcpyAsync(c->ctl_host, c->ctl, sizeof h, hipMemcpyDeviceToHost, st));
+    SQ_HIP(hipMemcpyAsync(c->fr_stable_h, c->fr_stable, sizeof(int) * (size_t)m, hipMemcpyDeviceToHost, st));
+    SQ_HIP(hipMemcpyAsync(c->fr_dtau_h, c->fr_dtau, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost, st));
+    SQ_HIP(hipMemcpyAsync(c->frame_host, c->rec_dev, 3 * sizeof(float) * (size_t)L, hipMemcpyDeviceToHost, st));
+    SQ_HIP(hipStreamSynchronize(st));
+    for (int i = 0; i < m; ++i) {
+        stable[f + i] = c->fr_stable_h[i];
+        if (dtau_out) dtau_out[f + i] = c->fr_dtau_h[i];
+    }
+    c->dtau = h.dtau;
+    c->stab_cnt = h.stab_cnt;
+    c->stab_T = h.T;
+    c->stab_V = h.V;
+    c->stab_fired = h.fired;
+    const float *r = static_cast<const float *>(c->frame_host);
+    c->rec_M.assign(r, r + L);
+    c->rec_D.assign(r + L, r + 2 * L);
+    c->rec_A.assign(r + 2 * L, r + 3 * L);
+    return SQ_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1560,6 +1678,13 @@ int sq_destroy(sq_ctx *c) {
         (void)hipFree(c->st_a);
     }
     if (c->frame_host) (void)hipHostFree(c->frame_host);
+    (void)hipFree(c->ctl);
+    (void)hipFree(c->rec_dev);
+    (void)hipFree(c->fr_stable);
+    (void)hipFree(c->fr_dtau);
+    if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+    if (c->fr_stable_h) (void)hipHostFree(c->fr_stable_h);
+    if (c->fr_dtau_h) (void)hipHostFree(c->fr_dtau_h);
     (void)hipFree(c->dacc);
     (void)hipFree(c->dpart);
     (void)hipFree(c->dslice);
@@ -1672,9 +1797,34 @@ int sq_run_frame(sq_ctx *c, int *stable) {
     if (!c || !stable) return fail(SQ_E_ARG, "null argument");
     DeviceGuard g(c->dev);
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = is_phi4(c) ? phi4_frame(c, stable) : qm1d_frame(c, stable);
+    int rc;
+    if (is_phi4(c)) {
+        rc = phi4_frames_dev(c, 1, stable, nullptr);
+    } else {
+        rc = qm1d_frame(c, stable);
+        if (!rc) adapt(c, *stable);
+    }
     if (rc) return rc;
-    adapt(c, *stable);
+    c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SQ_OK;
+}
+
+int sq_run_frames(sq_ctx *c, int nframes, int *stable, double *dtau) {
+    if (!c || (!stable && nframes > 0)) return fail(SQ_E_ARG, "null argument");
+    if (nframes < 0) return fail(SQ_E_ARG, "nframes < 0");
+    DeviceGuard g(c->dev);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (is_phi4(c)) {
+        int rc = phi4_frames_dev(c, nframes, stable, dtau);
+        if (rc) return rc;
+    } else {
+        for (int f = 0; f < nframes; ++f) {
+            int rc = qm1d_frame(c, &stable[f]);
+            if (rc) return rc;
+            adapt(c, stable[f]);
+            if (dtau) dtau[f] = c->dtau;
+        }
+    }
     c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return SQ_OK;
 }

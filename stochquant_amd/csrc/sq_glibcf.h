@@ -18,6 +18,23 @@
 // argument the reference can pass and more (logf on every float of [0, 2)
 // and the specials, cosf on [-6.3, 6.3]).  cosf beyond |x| >= 120 (glibc's
 // Payne-Hanek branch) is not restated: the callers pass 2 * 3.1415 * u < 6.3.
+//
+// Provenance and licences (see also THIRD_PARTY_NOTICES.md at the repo root):
+// the 16-entry log table, the logf/cosf polynomial coefficients and the
+// 2/pi reduction constants below are numeric data reproduced from GNU C
+// Library 2.35, sysdeps/ieee754/flt-32/{e_logf_data.c, s_sincosf_data.c,
+// sincosf.h}.  glibc is licensed LGPL-2.1-or-later; these files were
+// contributed to it by Arm Ltd from Arm's optimized-routines project
+// (Copyright (c) 2017-2018 Arm Ltd, today distributed under MIT OR
+// Apache-2.0 WITH LLVM-exception).  The flt-32 directory's older routines
+// carry Sun Microsystems' fdlibm notice, reproduced here because glibc's
+// single-precision reduction derives from it:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely
+//   granted, provided that this notice is preserved.
+// The code in this header is a restatement (written for this project), not a
+// copy of glibc's sources; the constants are what make it bit-identical.
 #pragma once
 
 #include <stdint.h>

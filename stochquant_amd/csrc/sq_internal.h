@@ -61,8 +61,39 @@ struct Phi4StepArgs {
     // frames (nullable): the frame's first fused launch also stores its input's
     // interior planes here -- the rollback snapshot, without a copy kernel
     float *snap;
+    // frames under device control (nullable): {h, sig, sigq} of the frame, read
+    // by the frame instances at launch start (FrameCtl::coef; the controller
+    // kernel of the previous frame may have changed Δτ)
+    const float *dcoef;
 };
 constexpr int kStabSlots = 32;
+
+// Device-resident frame controller (sq_run_frames): the
+// stability rule's carried state, the Δτ controller (tauhost.c:523-541) and the
+// step coefficients the next frame's launches read, so frames run back to back
+// without a host decision between them.
+struct FrameCtl {
+    double dtau;     // the next frame's Δτ
+    double C;        // noise amplitude (sigma = C sqrt(2 Δτ))
+    float coef[4];   // {h, sig, sigq, 0} of the next frame, computed from dtau as phi4_base_args does
+    float T, V;      // stability rule: last step's max phi', running max |phi'| (never rolled back)
+    int stab_cnt;    // stable frames since the last Δτ change
+    int adapt;       // Δτ controller on
+    int stable;      // the last frame's verdict (1 stable)
+    int fired;       // its firing step, -1 none
+    int flag;        // its guard flag
+    int frames;      // frames decided since the context's controller was (re)loaded
+};
+// One-block controller after a frame: folds the frame's kStabSlots-slot records
+// (and clears them and the guard flag for the next frame), writes the per-step
+// maxima to rec (M[L] | D[L] | A[L]), applies the stability rule and the Δτ
+// controller, and, when non-null, the verdict to *stable_out and the new Δτ to
+// *dtau_out.
+hipError_t phi4_frame_ctl_launch(FrameCtl *ctl, unsigned long long *md, unsigned int *am, int *flag, int L,
+                                 float *rec, int *stable_out, double *dtau_out, hipStream_t s);
+// Rollback of an unstable frame: dst = snap (n floats, n % 4 == 0) unless the
+// controller's verdict is stable (then every block exits at once).
+hipError_t phi4_rollback_launch(const FrameCtl *ctl, float *dst, const float *snap, size_t n, hipStream_t s);
 constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2): box_muller_q's missing factor (sq_rng.h)
 
 struct Phi4Geom {

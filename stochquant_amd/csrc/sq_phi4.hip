@@ -569,10 +569,28 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, FrameA
     }
 }
 
+// Frames under device control (Phi4StepArgs::dcoef): the step coefficients
+// come from the frame controller's state, which the previous frame's
+// controller kernel may have changed (the Δτ adapt of tauhost.c:523-541);
+// everything else from the launch.
+template <bool FR>
+__device__ __forceinline__ Phi4StepArgs frame_args(const Phi4StepArgs &A0) {
+    Phi4StepArgs A = A0;
+    if constexpr (FR) {
+        if (A0.dcoef != nullptr) {
+            A.h = A0.dcoef[0];
+            A.sig = A0.dcoef[1];
+            A.sigq = A0.dcoef[2];
+        }
+    }
+    return A;
+}
+
 // FR: a frame's launch (guard flag and stability records); the raw sq_step
 // path compiles without that bookkeeping.
 template <int QX, int R, int V, bool MS, bool NZ, int PF, bool FR>
-__global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A) {
+__global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A0) {
+    const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
     // the unit is wave-uniform: say so, so every descriptor stays scalar (T20)
@@ -796,7 +814,8 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 // (profiles/r01/fuse2_sweep.log).
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
-__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A) {
+__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
+    const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
     // one XCD: the blocks sharing halo rows, edge columns and chunk-edge planes
@@ -1062,7 +1081,8 @@ __device__ __forceinline__ void tp_xhalo(const Phi4StepArgs &A, const TbCtx &K, 
 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
-__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A) {
+__attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A0) {
+    const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
     const int yb = lb % A.nyg, rest = lb / A.nyg;
@@ -1214,6 +1234,87 @@ __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
     return v;
+}
+
+// ------------------------------------------------ device frame control ----
+// After each frame of sq_run_frames (sq_api.cpp phi4_frames_dev): the host
+// loop of phi4_frame (record fold, stab_rule, tauhost.c:523-541's Δτ rule)
+// restated for one block, so the next frame is enqueued without a host
+// decision.  The comparisons, the max and the double Δτ arithmetic are the
+// host's, operation for operation (bit-identical verdicts, Δτ and
+// coefficients: tests/test_gpu_phi4.py::test_run_frames_*).
+__device__ __forceinline__ float unord_f32_dev(uint32_t o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
+}
+
+__global__ __launch_bounds__(256) void phi4_frame_ctl_kernel(FrameCtl *ctl, unsigned long long *md,
+                                                             unsigned int *am, int *flag, int L, float *rec,
+                                                             int *stable_out, double *dtau_out) {
+    for (int j = threadIdx.x; j < L; j += blockDim.x) {
+        unsigned long long k = 0;
+        unsigned int a = 0;
+        for (int i = 0; i < kStabSlots; ++i) {
+            const size_t q = (size_t)j * kStabSlots + i;
+            k = k < md[q] ? md[q] : k;
+            a = a < am[q] ? am[q] : a;
+            md[q] = 0;  // cleared for the next frame (this thread is the slot's only reader)
+            am[q] = 0;
+        }
+        rec[j] = unord_f32_dev((uint32_t)(k >> 32));
+        rec[L + j] = __uint_as_float((uint32_t)k);
+        rec[2 * L + j] = __uint_as_float(a);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    const int h = *flag;
+    *flag = 0;
+    float T = ctl->T, V = ctl->V;
+    int fired = -1;
+    for (int j = 0; j < L; ++j) {  // stab_rule (sq_api.cpp)
+        const float M = rec[j], D = rec[L + j], Am = rec[2 * L + j];
+        const bool f = M > T && D > V;
+        T = M;
+        V = V < Am ? Am : V;
+        if (f) {
+            fired = j;
+            break;
+        }
+    }
+    ctl->T = T;
+    ctl->V = V;
+    ctl->fired = fired;
+    ctl->flag = h;
+    const int st = (h == 0 && fired < 0) ? 1 : 0;
+    ctl->stable = st;
+    ctl->frames += 1;
+    double dt = ctl->dtau;
+    if (ctl->adapt) {  // adapt (sq_api.cpp), tauhost.c:523-529,537-541
+        if (st) {
+            if (ctl->stab_cnt > 10) {
+                ctl->stab_cnt = 0;
+                dt /= 0.950;
+            }
+            ctl->stab_cnt += 1;
+        } else {
+            dt *= 0.950;
+            ctl->stab_cnt = 0;
+        }
+    }
+    ctl->dtau = dt;
+    const float hf = (float)dt;  // phi4_base_args
+    ctl->coef[0] = hf;
+    ctl->coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * ctl->C);
+    ctl->coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * ctl->C * kSqrt2Ln2);
+    if (stable_out) *stable_out = st;
+    if (dtau_out) *dtau_out = dt;
+}
+
+__global__ __launch_bounds__(256) void phi4_rollback_kernel(const FrameCtl *ctl, float4 *dst, const float4 *src,
+                                                            long long n4) {
+    if (ctl->stable) return;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * blockDim.x)
+        dst[i] = src[i];
 }
 
 // Per-block partials (no atomics: 1024 blocks' double atomics on one address
@@ -1446,9 +1547,13 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     const void *fn;
     // one 32-bit (signed, < 2^31 B) descriptor per padded buffer when it fits
     const bool wh = (long long)(a.nz + 2 * a.gz) * a.Lx * a.Ly * 4 < (1ll << 31);
-    // SQ_TB2_PIPE=0: the round-2 kernel (loads consumed in the iteration that issues them)
+    // the pipelined kernel (loads one plane iteration ahead) for rows wider than
+    // 256 sites, where it is 10 % faster at 512^3 (139-140 vs 155-156 us/step);
+    // the round-2 kernel (loads consumed in the iteration that issues them) for
+    // 256-site rows, where it is 6 % faster at 256^3 (16.8-17.0 vs 17.8-18.0:
+    // profiles/r03/ab).  SQ_TB2_PIPE=0 / 1 pins either.
     const char *pe = getenv("SQ_TB2_PIPE");  // read per launch (tests switch it within a process)
-    const bool pipe = pe ? atoi(pe) != 0 : true;
+    const bool pipe = pe ? atoi(pe) != 0 : wide;
 #define SQ_TB2K(N, W, E, F, H) (pipe ? (const void *)&phi4_tb2p_kernel<N, W, E, F, H> \
                                      : (const void *)&phi4_tb2_kernel<N, W, E, F, H>)
 #define SQ_TB2F(N, W, E, F) (wh ? SQ_TB2K(N, W, E, F, true) : SQ_TB2K(N, W, E, F, false))
@@ -1457,8 +1562,12 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
         fn = nz ? SQ_TB2(true, true, 6) : SQ_TB2(false, true, 6);
     else if (wide)
         fn = nz ? SQ_TB2(true, true, 1) : SQ_TB2(false, true, 1);
+    else if (fr)  // 78 VGPRs (unconstrained: 81, 88 allocated, 5 waves per SIMD: two 10-wave blocks
+                  // fit a CU only when the second one's waves land 2-2-3-3 against the first's
+                  // 3-3-2-2; frame launches 53 vs 45 us at 256^3)
+        fn = nz ? SQ_TB2F(true, false, 6, true) : SQ_TB2F(false, false, 6, true);
     else
-        fn = nz ? SQ_TB2(true, false, 1) : SQ_TB2(false, false, 1);
+        fn = nz ? SQ_TB2F(true, false, 1, false) : SQ_TB2F(false, false, 1, false);
 #undef SQ_TB2
 #undef SQ_TB2F
 #undef SQ_TB2K
@@ -1474,6 +1583,23 @@ hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, 
     const unsigned grid = (unsigned)std::min<size_t>((nq + 255) / 256, 8192);
     hipLaunchKernelGGL(phi4_init_kernel, dim3(grid), dim3(256), 0, s, slab, Lx, Ly, nz, zg0, k0, k1,
                        amp);
+    return hipGetLastError();
+}
+
+hipError_t phi4_frame_ctl_launch(FrameCtl *ctl, unsigned long long *md, unsigned int *am, int *flag, int L,
+                                 float *rec, int *stable_out, double *dtau_out, hipStream_t s) {
+    if (L < 1 || !ctl || !md || !am || !flag || !rec) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(phi4_frame_ctl_kernel, dim3(1), dim3(256), 0, s, ctl, md, am, flag, L, rec, stable_out,
+                       dtau_out);
+    return hipGetLastError();
+}
+
+hipError_t phi4_rollback_launch(const FrameCtl *ctl, float *dst, const float *snap, size_t n, hipStream_t s) {
+    if (n % 4 != 0) return hipErrorInvalidValue;
+    const long long n4 = (long long)(n / 4);
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, 1024));
+    hipLaunchKernelGGL(phi4_rollback_kernel, dim3(grid), dim3(256), 0, s, ctl, reinterpret_cast<float4 *>(dst),
+                       reinterpret_cast<const float4 *>(snap), n4);
     return hipGetLastError();
 }
 

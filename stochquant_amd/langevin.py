@@ -84,6 +84,17 @@ class _Ctx:
         _lib.call("sq_run_frame", self._h, ctypes.byref(st))
         return st.value == 1
 
+    def run_frames(self, n):
+        """n frames back to back (sq_run_frames: for phi^4 the verdict, rollback
+        and Δτ controller stay on the device); returns (stable bool array, Δτ
+        after each frame)."""
+        import numpy as np
+        st = np.zeros(max(n, 1), dtype=np.int32)
+        dt = np.zeros(max(n, 1), dtype=np.float64)
+        _lib.call("sq_run_frames", self._h, int(n), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int)),
+                  dt.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        return st[:n] == 1, dt[:n]
+
     def set_profiling(self, mode=1):
         """0 off; 1 every step kernel timed by dispatch events; 2 one event pair per step() call."""
         _lib.call("sq_set_profiling", self._h, int(mode))

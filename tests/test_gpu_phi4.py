@@ -834,3 +834,74 @@ def test_frame_launches_equal_raw_steps_repeated(gpu, oracle_mod, monkeypatch, p
     ref = run(False)
     for _ in range(8):
         assert np.array_equal(run(True), ref)
+
+
+RUN_FRAMES_CASES = [((256, 16, 16), 6, {}), ((256, 8, 12), 5, {}), ((64, 16, 8), 6, {}),
+                    ((512, 8, 6), 4, {}), ((256, 8, 12), 6, {"comm": "loopback", "nslabs": 3})]
+
+
+@pytest.mark.parametrize("shape,loops,kw", RUN_FRAMES_CASES)
+def test_run_frames_match_host_frames(gpu, oracle_mod, monkeypatch, shape, loops, kw):
+    """sq_run_frames (verdict, rollback and Δτ controller on the device between
+    frames) and sq_run_frame per frame equal the host-decided
+    frames (SQ_FRAME_HOST=1: record read-back, stab_rule and adapt on the host)
+    bit for bit: verdicts, the Δτ after every frame, the field, the carried
+    T / V and the last frame's records.  Δτ starts above the Euler limit, so
+    the run mixes rolled-back frames (Δτ x 0.95) with stable ones (Δτ / 0.95
+    after 11); fused (even and odd frame lengths), per-step, 512-wide and
+    multi-slab (host path) contexts."""
+    nfr = 40
+
+    def run(mode):
+        monkeypatch.setenv("SQ_FRAME_HOST", "1" if mode == "host" else "0")
+        with _lat(shape, C=1.0, dtau=0.19, m2=1.0, lam=1.0, seed=99, loops=loops, **kw) as L:
+            L.init_field(0.3)
+            if mode == "batch":
+                st, dt = L.run_frames(nfr)
+            else:
+                st, dt = [], []
+                for _ in range(nfr):
+                    st.append(L.run_frame())
+                    dt.append(L.dtau)
+                st, dt = np.array(st), np.array(dt)
+            return st, dt, L.download(), L.stability(), L.step_counter
+
+    ref = run("host")
+    assert ref[0].any() and not ref[0].all(), ref[0]
+    for mode in ("batch", "single"):
+        got = run(mode)
+        assert np.array_equal(got[0], ref[0]), mode
+        assert np.array_equal(got[1], ref[1]), mode
+        assert np.array_equal(got[2], ref[2]), mode
+        for k in ("M", "D", "A"):
+            assert np.array_equal(got[3][k], ref[3][k]), (mode, k)
+        for k in ("fired", "T", "V"):
+            assert got[3][k] == ref[3][k], (mode, k)
+        assert got[4] == ref[4] == nfr * loops
+
+
+def test_run_frames_after_upload_and_in_pieces(gpu, oracle_mod, monkeypatch):
+    """A field uploaded by the caller (not yet through the guard) runs its first
+    frame on the host path, the rest on the device; batches split anywhere
+    (and a caller's Δτ / stability state set between them) give the frames of
+    one batch."""
+    shape, loops = (256, 8, 16), 4
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+
+    def run(pieces):
+        with _lat(shape, C=1.0, dtau=0.19, m2=1.0, lam=1.0, seed=5, loops=loops) as L:
+            L.upload(phi0)
+            st, dt = [], []
+            for n in pieces:
+                s, d = L.run_frames(n)
+                st += list(s)
+                dt += list(d)
+            return np.array(st), np.array(dt), L.download(), L.dtau
+
+    a = run([30])
+    b = run([1, 7, 0, 13, 9])
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert a[3] == b[3] == a[1][-1]
+    monkeypatch.setenv("SQ_FRAME_HOST", "1")
+    c = run([30])
+    assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1]) and np.array_equal(a[2], c[2])
