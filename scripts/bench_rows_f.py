@@ -43,7 +43,7 @@ def main():
         lat.sync()
         raw = timed(lambda: lat.step(a.loops), a.reps, lat.sync)
         frame = timed(lambda: lat.run_frame(), a.reps, lat.sync)
-        batch = timed(lambda: lat.run_frames(a.reps), 3, lat.sync) / a.reps
+        batch = timed(lambda: lat.run_frames(100), 3, lat.sync) / 100
         os.environ["SQ_FRAME_HOST"] = "1"
         host = timed(lambda: lat.run_frame(), a.reps, lat.sync)
         del os.environ["SQ_FRAME_HOST"]
@@ -55,7 +55,7 @@ def main():
                           "batch_overhead_frac": round(batch / raw - 1, 4),
                           "host_decided_frame_us": round(host * 1e6, 1),
                           "note": "frame: sq_run_frame (device controller, one sync per frame); batch: "
-                                  "sq_run_frames(reps) per frame; host_decided: SQ_FRAME_HOST=1"}), flush=True)
+                                  "sq_run_frames(100) per frame; host_decided: SQ_FRAME_HOST=1"}), flush=True)
         mom = timed(lambda: lat.moments(), a.reps, lat.sync)
         cor = timed(lambda: lat.correlator(), a.reps, lat.sync)
         print(json.dumps({"row": "f2 observables", "moments_us": round(mom * 1e6, 1),

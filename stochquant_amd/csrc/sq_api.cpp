@@ -192,7 +192,9 @@ struct sq_ctx {
     unsigned int *st_a = nullptr;
     // phi^4 frames: st_md | st_a | flag in ONE device block (one memset, one
     // read-back per frame) and its pinned host mirror
-    void *frame_rec = nullptr;
+    void *frame_rec = nullptr;  // two record sets of frame_bytes (device frames alternate them)
+    void *frame_cur = nullptr;  // the active set (st_md, st_a, flag point into it)
+    int rec_set = 0;
     void *frame_host = nullptr;
     size_t frame_bytes = 0;
     bool frame_rec_zero = true;  // frame_rec is (or is queued to be) all zero: the next frame skips its memset
@@ -204,12 +206,13 @@ struct sq_ctx {
     // device frame control (phi4_frames_dev): controller state and its pinned
     // mirror, the last frame's folded records (M | D | A, loops floats each) and
     // per-frame verdicts / Δτ of a batch (fr_cap entries, device and pinned)
-    sq::FrameCtl *ctl = nullptr, *ctl_host = nullptr;
+    sq::FrameCtl *ctl = nullptr, *ctl_host = nullptr;  // ctl: two states (frame f reads ctl[f&1], writes the other)
     float *rec_dev = nullptr;
     int *fr_stable = nullptr, *fr_stable_h = nullptr;
     double *fr_dtau = nullptr, *fr_dtau_h = nullptr;
     int fr_cap = 0;
-    bool dev_frames = false;  // the current frame's launches read {h, sig, sigq} from ctl->coef
+    bool dev_frames = false;  // the current frame's launches read {h, sig, sigq} from ctl_cur->coef
+    sq::FrameCtl *ctl_cur = nullptr;
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
@@ -357,7 +360,7 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
     a.flag = c->in_frame ? c->flag : nullptr;  // the guard flag only feeds a frame's rollback
     a.st_md = nullptr;
     a.st_a = nullptr;
-    a.dcoef = (c->in_frame && c->dev_frames) ? c->ctl->coef : nullptr;
+    a.dcoef = (c->in_frame && c->dev_frames) ? c->ctl_cur->coef : nullptr;
     if (c->in_frame && c->st_md != nullptr) {
         const size_t k = (size_t)(c->step - c->frame_step0) * sq::kStabSlots;
         a.st_md = c->st_md + k;
@@ -868,6 +871,17 @@ int phi4_join(sq_ctx *c) {
     return SQ_OK;
 }
 
+// Point st_md / st_a / flag at record set k of frame_rec (st_md | st_a | flag).
+void use_rec_set(sq_ctx *c, int k) {
+    const size_t nrec = (size_t)sq::kStabSlots * (size_t)std::max(c->p.loops, 0);
+    char *b = static_cast<char *>(c->frame_rec) + (size_t)k * c->frame_bytes;
+    c->rec_set = k;
+    c->frame_cur = b;
+    c->st_md = nrec > 0 ? reinterpret_cast<unsigned long long *>(b) : nullptr;
+    c->st_a = nrec > 0 ? reinterpret_cast<unsigned int *>(b + nrec * sizeof(unsigned long long)) : nullptr;
+    c->flag = reinterpret_cast<int *>(b + nrec * (sizeof(unsigned long long) + sizeof(unsigned int)));
+}
+
 int create_phi4(sq_ctx *c) {
     const sq_params &p = c->p;
     if (p.dims[0] <= 0 || p.dims[1] <= 0 || p.dims[2] <= 0 || p.dims[0] > (1 << 20) ||
@@ -991,15 +1005,10 @@ int create_phi4(sq_ctx *c) {
     {
         const size_t nrec = (size_t)sq::kStabSlots * (size_t)std::max(p.loops, 0);
         c->frame_bytes = nrec * (sizeof(unsigned long long) + sizeof(unsigned int)) + 2 * sizeof(int);
-        SQ_HIP(hipMalloc(&c->frame_rec, c->frame_bytes));
-        SQ_HIP(hipMemset(c->frame_rec, 0, c->frame_bytes));
+        SQ_HIP(hipMalloc(&c->frame_rec, 2 * c->frame_bytes));
+        SQ_HIP(hipMemset(c->frame_rec, 0, 2 * c->frame_bytes));
         SQ_HIP(hipHostMalloc(&c->frame_host, c->frame_bytes, hipHostMallocDefault));
-        char *b = static_cast<char *>(c->frame_rec);
-        if (nrec > 0) {
-            c->st_md = reinterpret_cast<unsigned long long *>(b);
-            c->st_a = reinterpret_cast<unsigned int *>(b + nrec * sizeof(unsigned long long));
-        }
-        c->flag = reinterpret_cast<int *>(b + nrec * (sizeof(unsigned long long) + sizeof(unsigned int)));
+        use_rec_set(c, 0);
     }
     SQ_HIP(hipMalloc(&c->dacc, 2 * sizeof(double)));
     SQ_HIP(hipMalloc(&c->dpart, 4 * sizeof(double) * sq::kMomBlocks));
@@ -1359,7 +1368,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     }
     const size_t nrec = (size_t)sq::kStabSlots * (size_t)c->p.loops;
     if (!c->frame_rec_zero)  // records and guard flag (normally cleared behind the previous read-back)
-        SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, c->slabs[0].sA));
+        SQ_HIP(hipMemsetAsync(c->frame_cur, 0, c->frame_bytes, c->slabs[0].sA));
     c->frame_rec_zero = false;
     // frame-start snapshot, kept on device: a one-stream frame that starts
     // with a fused pair has that launch store its input's interior (every
@@ -1395,9 +1404,9 @@ int phi4_frame(sq_ctx *c, int *stable) {
         if (rc) return rc;
     }
     // one read-back of the records and the flag into pinned memory
-    SQ_HIP(hipMemcpyAsync(c->frame_host, c->frame_rec, c->frame_bytes, hipMemcpyDeviceToHost, s0.sA));
+    SQ_HIP(hipMemcpyAsync(c->frame_host, c->frame_cur, c->frame_bytes, hipMemcpyDeviceToHost, s0.sA));
     // clear the records for the next frame behind the read-back (stream order), off its start
-    SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, s0.sA));
+    SQ_HIP(hipMemsetAsync(c->frame_cur, 0, c->frame_bytes, s0.sA));
     c->frame_rec_zero = true;
     SQ_HIP(hipStreamSynchronize(s0.sA));
     const char *hb = static_cast<const char *>(c->frame_host);
@@ -1447,7 +1456,8 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     const int L = c->p.loops;
     const bool one_stream = c->slabs.size() == 1 && c->p.comm == SQ_COMM_NONE;
     const char *fh = getenv("SQ_FRAME_HOST");
-    const bool host_only = !one_stream || L < 1 || c->st_md == nullptr || (fh && atoi(fh) != 0);
+    const bool host_only = !one_stream || L < 1 || c->st_md == nullptr || (fh && atoi(fh) != 0) ||
+                           ((size_t)c->slabs[0].nz * plane_floats(c)) % 4 != 0;
     int f = 0;
     while (f < n && (host_only || !c->field_finite)) {  // host path (rollback restores fin0 = false)
         int rc = phi4_frame(c, &stable[f]);
@@ -1466,7 +1476,7 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         c->stab_init = true;
     }
     if (!c->ctl) {
-        SQ_HIP(hipMalloc(&c->ctl, sizeof(sq::FrameCtl)));
+        SQ_HIP(hipMalloc(&c->ctl, 2 * sizeof(sq::FrameCtl)));
         SQ_HIP(hipHostMalloc(&c->ctl_host, sizeof(sq::FrameCtl), hipHostMallocDefault));
         SQ_HIP(hipMalloc(&c->rec_dev, 3 * sizeof(float) * (size_t)L));
     }
@@ -1500,8 +1510,9 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     h.stable = 1;
     h.fired = -1;
     SQ_HIP(hipMemcpyAsync(c->ctl, c->ctl_host, sizeof h, hipMemcpyHostToDevice, st));
-    if (!c->frame_rec_zero) SQ_HIP(hipMemsetAsync(c->frame_rec, 0, c->frame_bytes, st));
-    c->frame_rec_zero = true;  // every controller launch leaves the records and the flag zero
+    // the active record set must start zero; each frame-end launch clears the
+    // other one, which the next frame then uses
+    if (!c->frame_rec_zero) SQ_HIP(hipMemsetAsync(c->frame_cur, 0, c->frame_bytes, st));
     const bool snap_in_kernel = c->tbz > 0 && L >= 2;
     for (int i = 0; i < m; ++i) {
         if (snap_in_kernel)
@@ -1510,18 +1521,36 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
             SQ_HIP(hipMemcpyAsync(s0.snap, plane0(c, s0, c->cur), nfl * sizeof(float), hipMemcpyDeviceToDevice, st));
         c->in_frame = true;
         c->dev_frames = true;
+        c->ctl_cur = c->ctl + (i & 1);
         c->frame_step0 = c->step;
         int rc = phi4_steps(c, L);
         c->in_frame = false;
         c->dev_frames = false;
         c->snap_next = nullptr;
         if (rc) return rc;
-        SQ_HIP(sq::phi4_frame_ctl_launch(c->ctl, c->st_md, c->st_a, c->flag, L, c->rec_dev, c->fr_stable + i,
-                                         c->fr_dtau + i, st));
-        SQ_HIP(sq::phi4_rollback_launch(c->ctl, plane0(c, s0, c->cur), s0.snap, nfl, st));
-        c->perf.kernel_launches += 2;
+        sq::FrameEndArgs e{};
+        e.cin = c->ctl + (i & 1);
+        e.cout = c->ctl + ((i + 1) & 1);
+        e.md = c->st_md;
+        e.am = c->st_a;
+        e.flag = c->flag;
+        const int cur_set = c->rec_set;
+        use_rec_set(c, cur_set ^ 1);
+        e.md_next = c->st_md;
+        e.am_next = c->st_a;
+        e.flag_next = c->flag;
+        e.L = L;
+        e.rec = c->rec_dev;
+        e.stable_out = c->fr_stable + i;
+        e.dtau_out = c->fr_dtau + i;
+        e.dst = reinterpret_cast<float4 *>(plane0(c, s0, c->cur));
+        e.snap = reinterpret_cast<const float4 *>(s0.snap);
+        e.n4 = (long long)(nfl / 4);
+        SQ_HIP(sq::phi4_frame_end_launch(e, st));
+        c->perf.kernel_launches += 1;
     }
-    SQ_HIP(hipMemcpyAsync(c->ctl_host, c->ctl, sizeof h, hipMemcpyDeviceToHost, st));
+    c->frame_rec_zero = true;  // the active set is the one the last frame-end launch cleared
+    SQ_HIP(hipMemcpyAsync(c->ctl_host, c->ctl + (m & 1), sizeof h, hipMemcpyDeviceToHost, st));
     SQ_HIP(hipMemcpyAsync(c->fr_stable_h, c->fr_stable, sizeof(int) * (size_t)m, hipMemcpyDeviceToHost, st));
     SQ_HIP(hipMemcpyAsync(c->fr_dtau_h, c->fr_dtau, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost, st));
     SQ_HIP(hipMemcpyAsync(c->frame_host, c->rec_dev, 3 * sizeof(float) * (size_t)L, hipMemcpyDeviceToHost, st));
@@ -1797,14 +1826,12 @@ int sq_run_frame(sq_ctx *c, int *stable) {
     if (!c || !stable) return fail(SQ_E_ARG, "null argument");
     DeviceGuard g(c->dev);
     const auto t0 = std::chrono::steady_clock::now();
-    int rc;
-    if (is_phi4(c)) {
-        rc = phi4_frames_dev(c, 1, stable, nullptr);
-    } else {
-        rc = qm1d_frame(c, stable);
-        if (!rc) adapt(c, *stable);
-    }
+    // one frame: the host-decided path (one read-back, 454 vs 478 us per 256^3
+    // 20-step frame for the device controller's state upload and read-back);
+    // sq_run_frames keeps the decisions on the device across frames
+    int rc = is_phi4(c) ? phi4_frame(c, stable) : qm1d_frame(c, stable);
     if (rc) return rc;
+    adapt(c, *stable);
     c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return SQ_OK;
 }

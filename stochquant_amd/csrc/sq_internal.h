@@ -84,16 +84,31 @@ struct FrameCtl {
     int flag;        // its guard flag
     int frames;      // frames decided since the context's controller was (re)loaded
 };
-// One-block controller after a frame: folds the frame's kStabSlots-slot records
-// (and clears them and the guard flag for the next frame), writes the per-step
-// maxima to rec (M[L] | D[L] | A[L]), applies the stability rule and the Δτ
-// controller, and, when non-null, the verdict to *stable_out and the new Δτ to
-// *dtau_out.
-hipError_t phi4_frame_ctl_launch(FrameCtl *ctl, unsigned long long *md, unsigned int *am, int *flag, int L,
-                                 float *rec, int *stable_out, double *dtau_out, hipStream_t s);
-// Rollback of an unstable frame: dst = snap (n floats, n % 4 == 0) unless the
-// controller's verdict is stable (then every block exits at once).
-hipError_t phi4_rollback_launch(const FrameCtl *ctl, float *dst, const float *snap, size_t n, hipStream_t s);
+// One launch after a frame (phi4_frame_end_kernel): folds the frame's
+// kStabSlots-slot records (md, am, flag), writes the per-step maxima to rec
+// (M[L] | D[L] | A[L]), applies the stability rule and the Δτ controller to
+// *cin and writes the result to *cout (cout->coef: the next frame's
+// coefficients), clears the other record set (md_next, am_next, flag_next)
+// for the next frame, writes the verdict to *stable_out and the new Δτ to
+// *dtau_out when non-null, and, unstable, copies snap back to dst (n4 float4).
+struct FrameEndArgs {
+    const FrameCtl *cin;
+    FrameCtl *cout;
+    const unsigned long long *md;
+    const unsigned int *am;
+    const int *flag;
+    unsigned long long *md_next;
+    unsigned int *am_next;
+    int *flag_next;
+    int L;
+    float *rec;
+    int *stable_out;
+    double *dtau_out;
+    float4 *dst;
+    const float4 *snap;
+    long long n4;
+};
+hipError_t phi4_frame_end_launch(const FrameEndArgs &e, hipStream_t s);
 constexpr double kSqrt2Ln2 = 1.1774100225154747;  // sqrt(2 ln 2): box_muller_q's missing factor (sq_rng.h)
 
 struct Phi4Geom {

@@ -1237,84 +1237,113 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ------------------------------------------------ device frame control ----
-// After each frame of sq_run_frames (sq_api.cpp phi4_frames_dev): the host
-// loop of phi4_frame (record fold, stab_rule, tauhost.c:523-541's Δτ rule)
-// restated for one block, so the next frame is enqueued without a host
-// decision.  The comparisons, the max and the double Δτ arithmetic are the
-// host's, operation for operation (bit-identical verdicts, Δτ and
-// coefficients: tests/test_gpu_phi4.py::test_run_frames_*).
+// After each frame of sq_run_frames (sq_api.cpp phi4_frames_dev), one launch:
+// the host loop of phi4_frame (record fold, stab_rule, tauhost.c:523-541's Δτ
+// rule) and its rollback, so the next frame is enqueued without a host
+// decision.  Every block folds the frame's records into LDS and takes the
+// verdict itself (a few KB of L2 reads per block, no grid-wide handoff); block
+// 0 writes the controller's next state (cout: the launches of the next frame
+// read cout->coef) and the folded records, and clears the other record set,
+// which the next frame accumulates into (the previous end launch read it);
+// when the verdict is unstable every block copies its share of the snapshot
+// back.  The comparisons, the max and the double Δτ arithmetic are the host's,
+// operation for operation (bit-identical verdicts, Δτ and coefficients:
+// tests/test_gpu_phi4.py::test_run_frames_*).
+constexpr int kEndChunk = 512;  // steps folded per LDS pass
+
 __device__ __forceinline__ float unord_f32_dev(uint32_t o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
-__global__ __launch_bounds__(256) void phi4_frame_ctl_kernel(FrameCtl *ctl, unsigned long long *md,
-                                                             unsigned int *am, int *flag, int L, float *rec,
-                                                             int *stable_out, double *dtau_out) {
-    for (int j = threadIdx.x; j < L; j += blockDim.x) {
-        unsigned long long k = 0;
-        unsigned int a = 0;
-        for (int i = 0; i < kStabSlots; ++i) {
-            const size_t q = (size_t)j * kStabSlots + i;
-            k = k < md[q] ? md[q] : k;
-            a = a < am[q] ? am[q] : a;
-            md[q] = 0;  // cleared for the next frame (this thread is the slot's only reader)
-            am[q] = 0;
+__global__ __launch_bounds__(256) void phi4_frame_end_kernel(FrameEndArgs E) {
+    __shared__ float sM[kEndChunk], sD[kEndChunk], sA[kEndChunk];
+    __shared__ float sT, sV;
+    __shared__ int sFired;
+    const bool b0 = blockIdx.x == 0;
+    if (threadIdx.x == 0) {
+        sT = E.cin->T;
+        sV = E.cin->V;
+        sFired = -1;
+    }
+    for (int j0 = 0; j0 < E.L; j0 += kEndChunk) {
+        const int n = min(kEndChunk, E.L - j0);
+        __syncthreads();  // sT / sV / sFired set, the previous chunk's rule done
+        for (int j = threadIdx.x; j < n; j += blockDim.x) {
+            unsigned long long k = 0;
+            unsigned int a = 0;
+            const size_t q0 = (size_t)(j0 + j) * kStabSlots;
+            for (int i = 0; i < kStabSlots; ++i) {
+                const unsigned long long mk = E.md[q0 + i];
+                const unsigned int ma = E.am[q0 + i];
+                k = k < mk ? mk : k;
+                a = a < ma ? ma : a;
+            }
+            sM[j] = unord_f32_dev((uint32_t)(k >> 32));
+            sD[j] = __uint_as_float((uint32_t)k);
+            sA[j] = __uint_as_float(a);
+            if (b0) {
+                E.rec[j0 + j] = sM[j];
+                E.rec[E.L + j0 + j] = sD[j];
+                E.rec[2 * E.L + j0 + j] = sA[j];
+            }
         }
-        rec[j] = unord_f32_dev((uint32_t)(k >> 32));
-        rec[L + j] = __uint_as_float((uint32_t)k);
-        rec[2 * L + j] = __uint_as_float(a);
+        __syncthreads();
+        if (threadIdx.x == 0 && sFired < 0) {  // stab_rule (sq_api.cpp); every chunk still folds (rec)
+            float T = sT, V = sV;
+            for (int j = 0; j < n; ++j) {
+                const bool f = sM[j] > T && sD[j] > V;
+                T = sM[j];
+                V = V < sA[j] ? sA[j] : V;
+                if (f) {
+                    sFired = j0 + j;
+                    break;
+                }
+            }
+            sT = T;
+            sV = V;
+        }
     }
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    const int h = *flag;
-    *flag = 0;
-    float T = ctl->T, V = ctl->V;
-    int fired = -1;
-    for (int j = 0; j < L; ++j) {  // stab_rule (sq_api.cpp)
-        const float M = rec[j], D = rec[L + j], Am = rec[2 * L + j];
-        const bool f = M > T && D > V;
-        T = M;
-        V = V < Am ? Am : V;
-        if (f) {
-            fired = j;
-            break;
-        }
-    }
-    ctl->T = T;
-    ctl->V = V;
-    ctl->fired = fired;
-    ctl->flag = h;
-    const int st = (h == 0 && fired < 0) ? 1 : 0;
-    ctl->stable = st;
-    ctl->frames += 1;
-    double dt = ctl->dtau;
-    if (ctl->adapt) {  // adapt (sq_api.cpp), tauhost.c:523-529,537-541
-        if (st) {
-            if (ctl->stab_cnt > 10) {
-                ctl->stab_cnt = 0;
-                dt /= 0.950;
+    const int st = (*E.flag == 0 && sFired < 0) ? 1 : 0;
+    if (b0) {
+        if (threadIdx.x == 0) {
+            FrameCtl c = *E.cin;
+            c.T = sT;
+            c.V = sV;
+            c.fired = sFired;
+            c.flag = *E.flag;
+            c.stable = st;
+            c.frames += 1;
+            if (c.adapt) {  // adapt (sq_api.cpp), tauhost.c:523-529,537-541
+                if (st) {
+                    if (c.stab_cnt > 10) {
+                        c.stab_cnt = 0;
+                        c.dtau /= 0.950;
+                    }
+                    c.stab_cnt += 1;
+                } else {
+                    c.dtau *= 0.950;
+                    c.stab_cnt = 0;
+                }
             }
-            ctl->stab_cnt += 1;
-        } else {
-            dt *= 0.950;
-            ctl->stab_cnt = 0;
+            const float hf = (float)c.dtau;  // phi4_base_args
+            c.coef[0] = hf;
+            c.coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C);
+            c.coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C * kSqrt2Ln2);
+            *E.cout = c;
+            if (E.stable_out) *E.stable_out = st;
+            if (E.dtau_out) *E.dtau_out = c.dtau;
+            *E.flag_next = 0;
+        }
+        for (long long q = threadIdx.x; q < (long long)E.L * kStabSlots; q += blockDim.x) {
+            E.md_next[q] = 0;
+            E.am_next[q] = 0;
         }
     }
-    ctl->dtau = dt;
-    const float hf = (float)dt;  // phi4_base_args
-    ctl->coef[0] = hf;
-    ctl->coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * ctl->C);
-    ctl->coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * ctl->C * kSqrt2Ln2);
-    if (stable_out) *stable_out = st;
-    if (dtau_out) *dtau_out = dt;
-}
-
-__global__ __launch_bounds__(256) void phi4_rollback_kernel(const FrameCtl *ctl, float4 *dst, const float4 *src,
-                                                            long long n4) {
-    if (ctl->stable) return;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+    if (st) return;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < E.n4;
          i += (long long)gridDim.x * blockDim.x)
-        dst[i] = src[i];
+        E.dst[i] = E.snap[i];
 }
 
 // Per-block partials (no atomics: 1024 blocks' double atomics on one address
@@ -1586,20 +1615,13 @@ hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, 
     return hipGetLastError();
 }
 
-hipError_t phi4_frame_ctl_launch(FrameCtl *ctl, unsigned long long *md, unsigned int *am, int *flag, int L,
-                                 float *rec, int *stable_out, double *dtau_out, hipStream_t s) {
-    if (L < 1 || !ctl || !md || !am || !flag || !rec) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(phi4_frame_ctl_kernel, dim3(1), dim3(256), 0, s, ctl, md, am, flag, L, rec, stable_out,
-                       dtau_out);
-    return hipGetLastError();
-}
-
-hipError_t phi4_rollback_launch(const FrameCtl *ctl, float *dst, const float *snap, size_t n, hipStream_t s) {
-    if (n % 4 != 0) return hipErrorInvalidValue;
-    const long long n4 = (long long)(n / 4);
-    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, 1024));
-    hipLaunchKernelGGL(phi4_rollback_kernel, dim3(grid), dim3(256), 0, s, ctl, reinterpret_cast<float4 *>(dst),
-                       reinterpret_cast<const float4 *>(snap), n4);
+hipError_t phi4_frame_end_launch(const FrameEndArgs &e, hipStream_t s) {
+    if (e.L < 1 || !e.cin || !e.cout || e.cin == e.cout || !e.md || !e.am || !e.flag || !e.md_next || !e.am_next ||
+        !e.flag_next || e.md == e.md_next || !e.rec || (e.n4 > 0 && (!e.dst || !e.snap)))
+        return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::max<long long>(1, std::min<long long>((e.n4 + 1023) / 1024, 512));
+    FrameEndArgs q = e;
+    hipLaunchKernelGGL(phi4_frame_end_kernel, dim3(grid), dim3(256), 0, s, q);
     return hipGetLastError();
 }
 
