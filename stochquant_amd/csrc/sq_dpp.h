@@ -55,14 +55,22 @@ __device__ __forceinline__ float dpp_f(float v, float id) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, id), __builtin_bit_cast(int, v),
                                                                  CTRL, RM, BM, false));
 }
+// v_max_f32 as is: fmaxf of a DPP-moved value (an integer move to the
+// compiler) gets a quieting v_max_f32 x, x, x first; the moved values here are
+// never signalling NaNs
+__device__ __forceinline__ float dpp_vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 __device__ __forceinline__ float dpp_all_max_f(float v) {  // wave maximum (no NaN inputs), wave-uniform
     const float id = -__builtin_inff();
-    v = fmaxf(v, dpp_f<0x111, 0xf, 0xf>(v, id));
-    v = fmaxf(v, dpp_f<0x112, 0xf, 0xf>(v, id));
-    v = fmaxf(v, dpp_f<0x114, 0xf, 0xf>(v, id));
-    v = fmaxf(v, dpp_f<0x118, 0xf, 0xf>(v, id));
-    v = fmaxf(v, dpp_f<0x142, 0xa, 0xf>(v, id));
-    v = fmaxf(v, dpp_f<0x143, 0xc, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x111, 0xf, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x112, 0xf, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x114, 0xf, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x118, 0xf, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x142, 0xa, 0xf>(v, id));
+    v = dpp_vmax(v, dpp_f<0x143, 0xc, 0xf>(v, id));
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
 }
 

@@ -159,10 +159,16 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
     const float cl = A.clampv;
     float4 o = make_float4(v0.x, v0.y, v1.x, v1.y);
     const float m = fmaxf(fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)), fabsf(o.w));  // v_max3 + v_max
-    if (mpre != nullptr) *mpre = m;  // frames: max |phi'| before the guard (frame_sites)
-    if (!fin || !(m < cl))
+    float mo = m;
+    if (!fin || !(m < cl)) {
         o = make_float4(fmaxf(fminf(o.x, cl), -cl), fmaxf(fminf(o.y, cl), -cl), fmaxf(fminf(o.z, cl), -cl),
                         fmaxf(fminf(o.w, cl), -cl));
+        if (mpre != nullptr) mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
+    }
+    // frames: max |phi'| of the returned float4 -- m itself where the guard had
+    // nothing to do (every |phi'| < clamp, finite), else taken after the guard
+    // (a NaN that fmaxf dropped from m is +clamp there)
+    if (mpre != nullptr) *mpre = mo;
     return o;
 }
 
@@ -171,14 +177,13 @@ __device__ __forceinline__ float4 site_update4(float4 c, float lft, float rgt, f
 // heuristic (tau_kernel.cl:135-143): m = max phi', d = the
 // drift increment |phi' - phi - sigma xi| at the sites attaining m (the
 // largest one on ties), mw = the wave's running maximum of phi'
-// (wave-uniform).  am: the running max |phi'| -- taken before the guard where
-// the inputs are known finite (site_update4's mpre: no NaN can hide from it),
-// after the guard otherwise; either way the guard flag is am >= clamp (the
-// guard clamps to [-clamp, clamp], so some site reached the clamp iff the
-// maximum did) and max |phi'| after the guard is min(am, clamp).  One
-// accumulator for both forms: round 2 kept the post-guard flag and maximum in
-// two more, and the compiler selected between their addresses through 12
-// bytes of private memory per lane.
+// (wave-uniform).  am: the running max |phi'| after the guard (site_update4's
+// mpre, or taken from o); the guard flag is am >= clamp (the guard clamps to
+// [-clamp, clamp], NaN to +clamp, so some site was clamped iff the maximum
+// reached the clamp) and max |phi'| after the guard is min(am, clamp) = am.
+// One accumulator: round 2 kept the flag and maximum in two more, and the
+// compiler selected between their addresses through 12 bytes of private
+// memory per lane.
 struct FrameAcc {
     float m, d;
     float mw;
@@ -188,10 +193,31 @@ __device__ __forceinline__ FrameAcc frame_acc() {
     return FrameAcc{-__builtin_inff(), 0.f, -__builtin_inff(), 0.f};
 }
 
+// v_max_f32 / v_max3_f32 without the IEEE-mode operand canonicalisation the
+// compiler wraps around fmaxf (a quieting v_max_f32 x, x, x per operand it
+// cannot prove canonical: 2 of the 4 instructions of a float4's max).  For
+// operands that are results of arithmetic, never signalling NaNs; a quiet NaN
+// operand still yields the other one, as fmaxf.
+__device__ __forceinline__ float vmax(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+// Branch-free: the larger drift increment on ties is computed up front and
+// selected (the selects of a conditional fmaxf compiled to exec-masked blocks).
 __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float xi, float sig) {
     const float dn = fabsf(__builtin_fmaf(-sig, xi, o - c));
-    f.d = o > f.m ? dn : (o == f.m ? fmaxf(f.d, dn) : f.d);
-    f.m = fmaxf(f.m, o);
+    const float dt = vmax(f.d, dn);
+    const bool gt = o > f.m, eq = o == f.m;
+    const float d1 = eq ? dt : f.d;
+    f.d = gt ? dn : d1;
+    f.m = vmax(f.m, o);
 }
 
 // The frame bookkeeping of one float4 of outputs o (inputs c, noise xi).
@@ -201,24 +227,24 @@ __device__ __forceinline__ void stab_site(FrameAcc &f, float o, float c, float x
 // maximum in about H(n) of its n planes): the lanes' (m, d) may then miss
 // sites below mw, but the wave's maximum key ord(m) << 32 | bits(d), all
 // that frame_flush keeps, is exact.  am (guard flag, max |phi'|) takes every site.
-// bw (the fused kernel): the block's running maximum of this record in LDS,
+// bw (BW, the fused kernels): the block's running maximum of this record in LDS,
 // raised by each wave that meets a new maximum of its own; the threshold is
 // then the larger of the two, still a value some site of the record attains,
 // so the block's key stays exact and a wave takes the per-site path about
 // 1 + H(n)/waves times instead of H(n).  Waves read it without
 // a barrier: any value read is a valid (monotone, attained) threshold.
-// pre: mpre is site_update4's pre-guard max |phi'| of o (finite inputs: no
-// NaN can hide from it), accumulated into am; otherwise the guarded o's.
-template <bool NZ>
+// pre: mpre is site_update4's max |phi'| of o (the fused kernels), accumulated
+// into am; otherwise taken from o here.
+template <bool NZ, bool BW = false>
 __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, const float4 &o, const float4 &c,
                                             const f32x4n &xi, float *bw = nullptr, bool pre = false,
                                             float mpre = 0.f) {
     const float mo = pre ? mpre : fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fmaxf(fabsf(o.z), fabsf(o.w)));
-    f.am = fmaxf(f.am, mo);
-    if (A.st_md != nullptr) {
-        const float o4 = fmaxf(fmaxf(o.x, o.y), fmaxf(o.z, o.w));
+    f.am = vmax(f.am, mo);  // mo: never a signalling NaN (arithmetic / the guard's output)
+    {  // frame launches always carry the records (the launchers check st_md, st_a)
+        const float o4 = vmax(vmax3(o.x, o.y, o.z), o.w);  // the guard's output: never NaN
         float t = f.mw;
-        if (bw != nullptr) t = fmaxf(t, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if constexpr (BW) t = vmax(t, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
         if (__ballot(o4 >= t) != 0ull) {
             const float s = NZ ? A.sigq : 0.f;
             stab_site(f, o.x, c.x, xi.a, s);
@@ -226,7 +252,7 @@ __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, 
             stab_site(f, o.z, c.z, xi.c, s);
             stab_site(f, o.w, c.w, xi.d, s);
             f.mw = dpp_all_max_f(f.m);
-            if (bw != nullptr && (threadIdx.x & 63) == 0)
+            if (BW && (threadIdx.x & 63) == 0)
                 __hip_atomic_fetch_max(bw, f.mw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
@@ -753,7 +779,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         float mp1;
         T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v, &mp1);
         if constexpr (FR) {
-            frame_sites<NZ>(A, f1, T2, I1.row, xa, bmx, A.fin != 0, mp1);
+            frame_sites<NZ, true>(A, f1, T2, I1.row, xa, bmx, true, mp1);
             // the frame's snapshot: each output row's input at its owned planes, once
             if (A.snap != nullptr && K.outw && p + 1 >= K.z0 && p + 1 < K.z1)
                 __builtin_nontemporal_store(
@@ -788,7 +814,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         // step s+1 reads step s's guarded output: always finite
         float mp2;
         const float4 o = site_update4<NZ>(T1, lft, rgt, up, dn, T0, T2, xb, A, true, K.m2v, &mp2);
-        if constexpr (FR) frame_sites<NZ>(A, f2, o, T1, xb, bmx + 1, true, mp2);
+        if constexpr (FR) frame_sites<NZ, true>(A, f2, o, T1, xb, bmx + 1, true, mp2);
         if constexpr (WH) {
             // the plane offset in the VGPR offset, soffset 0: see bstore4
             bstore4<17>(K.rout, K.voff + (uint32_t)(p - 1 + A.gz) * K.pbytes, o);
@@ -1013,7 +1039,7 @@ __device__ __forceinline__ void tp_row(const Phi4StepArgs &A, const TbCtx &K, Tp
     }
     float mp1;
     T[tc] = site_update4<NZ>(I[ic], lft, rgt, up, dn, I[im], I[ip], xa, A, A.fin != 0, K.m2v, &mp1);
-    if constexpr (FR) frame_sites<NZ>(A, f1, T[tc], I[ic], xa, bmx, A.fin != 0, mp1);
+    if constexpr (FR) frame_sites<NZ, true>(A, f1, T[tc], I[ic], xa, bmx, true, mp1);
     t_lds[sc][K.w][K.lane] = T[tc];
     // 4. B: step s+1 at plane k-1 from T(k-2), T(k-1), T(k) and T(k-1)'s
     //    y-neighbours, published in iteration k-1
@@ -1033,7 +1059,7 @@ __device__ __forceinline__ void tp_row(const Phi4StepArgs &A, const TbCtx &K, Tp
         }
         float mp2;
         o = site_update4<NZ>(T[tm], bl, br, bu, bd, T[tmm], T[tc], xb, A, true, K.m2v, &mp2);
-        if constexpr (FR) frame_sites<NZ>(A, f2, o, T[tm], xb, bmx + 1, true, mp2);
+        if constexpr (FR) frame_sites<NZ, true>(A, f2, o, T[tm], xb, bmx + 1, true, mp2);
     }
     if constexpr (WH) {
         bstore4<17>(K.rout, bw ? K.voff + (uint32_t)(k - 1 + A.gz) * K.pbytes : kTpOob, o);  // soffset 0: bstore4
@@ -1505,6 +1531,8 @@ static hipError_t launch_fr(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hip
 template <int QX, int R, int V, bool MS, bool NZ, int PF>
 static hipError_t launch_pf(const Phi4StepArgs &a, dim3 grid, hipStream_t s, hipEvent_t e0,
                             hipEvent_t e1) {
+    if (a.flag != nullptr && (a.st_md == nullptr || a.st_a == nullptr))
+        return hipErrorInvalidValue;  // frame launches carry the records (frame_sites)
     return a.flag != nullptr ? launch_fr<QX, R, V, MS, NZ, PF, true>(a, grid, s, e0, e1)
                              : launch_fr<QX, R, V, MS, NZ, PF, false>(a, grid, s, e0, e1);
 }
@@ -1573,6 +1601,7 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     const bool nz = a.sig != 0.0f;
     static const int wpe = getenv("SQ_TB2_WPE") ? atoi(getenv("SQ_TB2_WPE")) : 6;
     const bool fr = a.flag != nullptr;
+    if (fr && (a.st_md == nullptr || a.st_a == nullptr)) return hipErrorInvalidValue;  // frame_sites
     const void *fn;
     // one 32-bit (signed, < 2^31 B) descriptor per padded buffer when it fits
     const bool wh = (long long)(a.nz + 2 * a.gz) * a.Lx * a.Ly * 4 < (1ll << 31);
