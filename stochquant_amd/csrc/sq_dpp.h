@@ -51,6 +51,24 @@ __device__ __forceinline__ int dpp_all_max_i(int v) {
 }
 __device__ __forceinline__ int dpp_all_min_i(int v) { return -dpp_all_max_i(-v); }
 template <int CTRL, int RM, int BM>
+__device__ __forceinline__ unsigned long long dpp_max_step_u64(unsigned long long v) {
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)v, CTRL, RM, BM, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp(0, (int)(unsigned)(v >> 32), CTRL, RM, BM, false);
+    const unsigned long long w = ((unsigned long long)hi << 32) | lo;
+    return w > v ? w : v;
+}
+__device__ __forceinline__ unsigned long long dpp_all_max_u64(unsigned long long v) {  // wave-uniform
+    v = dpp_max_step_u64<0x111, 0xf, 0xf>(v);
+    v = dpp_max_step_u64<0x112, 0xf, 0xf>(v);
+    v = dpp_max_step_u64<0x114, 0xf, 0xf>(v);
+    v = dpp_max_step_u64<0x118, 0xf, 0xf>(v);
+    v = dpp_max_step_u64<0x142, 0xa, 0xf>(v);
+    v = dpp_max_step_u64<0x143, 0xc, 0xf>(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)v, 63);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+template <int CTRL, int RM, int BM>
 __device__ __forceinline__ float dpp_f(float v, float id) {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, id), __builtin_bit_cast(int, v),
                                                                  CTRL, RM, BM, false));

@@ -65,6 +65,7 @@ struct Phi4StepArgs {
     // by the frame instances at launch start (FrameCtl::coef; the controller
     // kernel of the previous frame may have changed Δτ)
     const float *dcoef;
+    int prio;  // fused kernels: wave priority by march progress (prio_by_progress)
 };
 constexpr int kStabSlots = 32;
 

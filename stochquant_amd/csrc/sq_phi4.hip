@@ -273,15 +273,9 @@ __device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAc
     const bool bad = f.am >= A.clampv;
     if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     if (A.st_md == nullptr) return;
-    uint64_t k = ((uint64_t)ord_f32(f.m) << 32) | __float_as_uint(f.d);
-    uint32_t a = __float_as_uint(fminf(f.am, A.clampv));
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint64_t k2 = __shfl_xor(k, o, 64);
-        const uint32_t a2 = __shfl_xor(a, o, 64);
-        k = k2 > k ? k2 : k;
-        a = a2 > a ? a2 : a;
-    }
+    // wave maxima by DPP scans (bits of non-negative floats order as ints)
+    uint64_t k = dpp_all_max_u64(((uint64_t)ord_f32(f.m) << 32) | __float_as_uint(f.d));
+    uint32_t a = (uint32_t)dpp_all_max_i((int)__float_as_uint(fminf(f.am, A.clampv)));
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
@@ -660,6 +654,22 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A0) {
 // z-1 neighbour read from a fourth LDS slot (90 VGPRs at S = 1, 109 at S > 1):
 // 256^3 21.4 -> 21.8 us per step, 512^3 197 -> 330 us -- the kernel is not
 // waiting on its loads.
+// Wave priority by march progress (Phi4StepArgs::prio): the two blocks that
+// share a CU start together, and the arbiter's age order lets one finish far
+// ahead, leaving the other alone on the CU for the rest of the launch (block
+// stamps: ends 20..36 us at 256^3, 19-20 us alone).  A block that is behind
+// gets the higher priority: 3 in its first quarter of planes, down to 0 in
+// its last (4 levels beat 2: 3 then 0 by halves, 512^3 139-140 vs 136-137
+// us/step).  q = quarter (0..3), wave-uniform.
+__device__ __forceinline__ void prio_by_progress(int q) {
+    switch (q) {
+    case 0: __builtin_amdgcn_s_setprio(3); break;
+    case 1: __builtin_amdgcn_s_setprio(2); break;
+    case 2: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+    }
+}
+
 constexpr int kTbRows = 8;
 constexpr int kTbWaves = kTbRows + 2;  // row waves; S > 1 adds the x-halo wave
 
@@ -932,7 +942,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
     R.qzm = 0;  // plane z0-2: no step s+1 output there
     // three-plane queues unrolled three ways so no rotation moves are emitted
+    const int span = z1 - K.z0 + 2;
     for (int p = K.z0 - 1; p <= z1; p += 3) {
+        if (A.prio) prio_by_progress(4 * (p - K.z0 + 1) / span);
         tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2, bmx);
         if (p + 1 > z1) break;
         tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2, bmx);
@@ -1203,7 +1215,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
         if (xrow) in_lds[0][xslot][K.lane] = X[0];
         T[0] = T[1] = T[2] = T[3] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
+        const int span = z1 - K.z0 + 2;
         for (int k = K.z0 - 1; k <= z1; k += 4) {
+            if (A.prio) prio_by_progress(4 * (k - K.z0 + 1) / span);
             tp_row<NZ, WIDE, FR, WH, 0>(A, K, R, k, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
             if (k + 1 > z1) break;
             tp_row<NZ, WIDE, FR, WH, 1>(A, K, R, k + 1, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
@@ -1220,7 +1234,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
         C[2] = bload1(p2, K.voff);
         NB[0] = make_float4(bload1(p1, K.vex), bload1(p1, K.vx2), bload1(p1, K.vm), bload1(p1, K.vp));
         __syncthreads();
+        const int span = z1 - K.z0 + 2;
         for (int k = K.z0 - 1; k <= z1; k += 4) {
+            if (A.prio) prio_by_progress(4 * (k - K.z0 + 1) / span);
             tp_xhalo<NZ, WH, 0>(A, K, R, k, C, NB, tx);
             if (k + 1 > z1) break;
             tp_xhalo<NZ, WH, 1>(A, K, R, k + 1, C, NB, tx);
@@ -1630,6 +1646,10 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
 #undef SQ_TB2F
 #undef SQ_TB2K
     Phi4StepArgs q = a;
+    // wave priority by march progress: 256^3 16.3-16.7 vs 17.0 us/step, 512^3
+    // 135-137 vs 140-141 (profiles/r03/prio); SQ_TB2_PRIO=0 turns it off
+    static const int prio = getenv("SQ_TB2_PRIO") ? atoi(getenv("SQ_TB2_PRIO")) : 1;
+    q.prio = prio;
     void *args[] = {&q};
     if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
     return hipLaunchKernel(fn, grid, block, args, 0, s);
