@@ -191,11 +191,16 @@ def cpu_baseline(L, dtau, target_s):
 def pmc_record(L, nranks, kernel):
     """The committed rocprofv3 PMC summary for this workload and kernel, if any (it is
     measured by scripts/pmc_r02.sh on this same command, not inside this run)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    try:
-        with open(path) as fh:
-            d = json.load(fh)
-    except (OSError, ValueError):
+    for name in (f"pmc_traffic_{L}.json", "pmc_traffic.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("size") == L:
+            break
+    else:
         return None, None
     k = kernel.split("<")[0]
     if d.get("size") == L and d.get("nranks", 1) == nranks and k and k in d.get("kernel", ""):
@@ -349,10 +354,34 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
         if tb:
             r["real_GBps"] = round(tb / (launch_ms * 1e-3) / 1e9, 1)
             r["frac_real"] = round(tb / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        for k in ("valu_util_simd", "valu_util_method", "busy_fraction", "busy_source", "pmc_kernel_us"):
+        for k in ("valu_util_simd", "valu_issue_util_simd", "avg_resident_waves_per_simd", "valu_util_method",
+                  "pmc_kernel_us"):
             if rec.get(k) is not None:
                 r[k] = rec[k]
+    if fused and not slab_path and world == 1:
+        r.update(busy_fraction(lat))
     return r, value, fused
+
+
+def busy_fraction(lat, reps=5):
+    """Launch busy fraction from per-block clock stamps of a few fused launches
+    (sq_phi4_block_stamps, measured in this run): the blocks' summed durations
+    over blocks x launch span (first start to last end), median of `reps`
+    launches; with the block-end percentiles (us from the launch's first start)."""
+    import numpy as np
+    fr, spans, ends = [], [], []
+    for _ in range(reps):
+        st, en = lat.block_stamps()
+        t0 = st.min()
+        span = float(en.max() - t0)
+        fr.append(float((en - st).sum()) / (len(st) * span))
+        spans.append(span * 1e-2)          # 100 MHz ticks -> us
+        ends.append(np.percentile((en - t0) * 1e-2, [10, 50, 90]))
+    i = int(np.argsort(fr)[len(fr) // 2])
+    return {"busy_fraction": round(fr[i], 3), "busy_launch_span_us": round(spans[i], 2),
+            "busy_block_end_us_p10_p50_p90": [round(float(x), 2) for x in ends[i]],
+            "busy_source": "sq_phi4_block_stamps: per-block s_memrealtime start/end of the fused launch, "
+                           f"median of {reps} launches in this run"}
 
 
 def cpu_baseline_c3(L, dtau, target_s):

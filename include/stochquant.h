@@ -255,6 +255,12 @@ int sq_set_profiling(sq_ctx *ctx, int mode);
 int sq_perf(sq_ctx *ctx, sq_perf_t *out);
 int sq_perf_reset(sq_ctx *ctx);
 int sq_sync(sq_ctx *ctx);
+/* PHI4, one slab without an exchange, fused launches: run the next two steps
+ * (one fused launch, as sq_step(ctx, 2)) with per-block stamps of the
+ * constant 100 MHz clock: out[2b], out[2b+1] = start / end of block b
+ * (cap >= blocks of the launch); *nblocks = blocks.  A measurement hook for
+ * the launch's ramp, tail and busy fraction (bench.py roofline). */
+int sq_phi4_block_stamps(sq_ctx *ctx, unsigned long long *out, int cap, int *nblocks);
 
 /* RCCL bootstrap: rank 0 creates the id, the caller distributes it (e.g. via
  * torch.distributed) into sq_params.comm_id of every rank. */

@@ -21,6 +21,9 @@ import json
 import os
 import statistics
 
+N_SIMD = 1024        # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4      # peak engine clock (MI355X_MICROARCH.md)
+
 
 def counter_values(d, counter, kernel_substr="phi4_"):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
@@ -84,19 +87,23 @@ def main():
         with open(a.sq) as fh:
             sq = json.load(fh)
         med, der = sq["median_per_launch"], sq["derived"]
-        waves_per_simd = None
-        if "SQ_WAVES" in med:
-            # resident waves per SIMD: the grid is one round of blocks (bench), so
-            # every wave is resident for (nearly) the whole launch
-            waves_per_simd = med["SQ_WAVES"] / 1024.0
-        act = der.get("SQ_ACTIVE_INST_VALU/WAVE_CYCLES")
         out["sq_source"] = a.sq
         out["valu_insts_per_wave"] = der.get("VALU_insts_per_wave")
-        out["valu_active_per_wave"] = act
-        out["waves_per_simd"] = waves_per_simd
-        # each SIMD's VALU issue is busy ~ waves x the fraction of a wave's cycles it issues VALU
-        out["valu_issue_frac"] = round(min(1.0, act * waves_per_simd), 3) if act and waves_per_simd else None
-        out["valu_issue_frac_by_grbm"] = der.get("VALU_issue_frac_at_4cyc")
+        dur = med.get("_duration_us")
+        if dur and "SQ_ACTIVE_INST_VALU" in med:
+            # per-SIMD VALU utilisation over the kernel span: the VALU issue
+            # cycles of all waves (SQ_ACTIVE_INST_VALU counts quad-cycles) over
+            # 1024 SIMDs x the launch's cycles at the 2.4 GHz peak engine clock
+            # (a lower bound if the clock ran below peak); issue-cost form: one
+            # wave64 VALU instruction = 4 cycles (SQ_INSTS_VALU x 4)
+            cyc = CLOCK_GHZ * 1e3 * dur
+            out["pmc_kernel_us"] = round(dur, 3)
+            out["valu_util_simd"] = round(4.0 * med["SQ_ACTIVE_INST_VALU"] / (N_SIMD * cyc), 3)
+            out["valu_issue_util_simd"] = round(4.0 * med["SQ_INSTS_VALU"] / (N_SIMD * cyc), 3)
+            if "SQ_WAVE_CYCLES" in med:
+                out["avg_resident_waves_per_simd"] = round(4.0 * med["SQ_WAVE_CYCLES"] / (N_SIMD * cyc), 2)
+            out["valu_util_method"] = (f"SQ_ACTIVE_INST_VALU x 4 / ({N_SIMD} SIMDs x {CLOCK_GHZ} GHz x "
+                                       f"kernel duration of the PMC run)")
     with open(a.out, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out))

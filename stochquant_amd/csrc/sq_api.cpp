@@ -174,6 +174,9 @@ struct sq_ctx {
     int *flag = nullptr;
     bool in_frame = false;  // phi4_frame: the step kernels raise the guard flag
     float *snap_next = nullptr;  // phi4_frame: the next fused launch writes its input here (Phi4StepArgs::snap)
+    unsigned long long *stamps_next = nullptr;  // sq_phi4_block_stamps: the next fused launch's block stamps
+    unsigned long long *dstamps = nullptr;
+    int stamps_cap = 0, stamps_blocks = 0;
     bool field_finite = true;  // every plane of the current field has been through the guard (or
                                // came from sq_init_field); false after a caller's upload / load
     bool fin_sync = false;     // multi-rank: field_finite changed locally; the next step call
@@ -414,6 +417,8 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     sq::Phi4StepArgs a = phi4_base_args(c, s, in_buf);
     a.snap = c->snap_next;  // only a one-stream frame's first launch (phi4_frame)
     c->snap_next = nullptr;
+    a.stamps = c->stamps_next;  // sq_phi4_block_stamps
+    c->stamps_next = nullptr;
     // planes per block: pinned, or as many as make one round of tb_blocks
     // blocks (a ragged second round costs more than the deeper chunks), but
     // not fewer than 4 (a chunk recomputes 2 planes of the first step)
@@ -437,6 +442,10 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
         int rc = ev_take(c, &e);
         if (rc) return rc;
         c->ev_extra_steps += 1;
+    }
+    if (a.stamps != nullptr) {
+        if (a.nunits > c->stamps_cap) return fail(SQ_E_STATE, "block stamps: more blocks than stamp slots");
+        c->stamps_blocks = a.nunits;
     }
     SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
     c->perf.kernel_launches += 1;
@@ -1708,6 +1717,7 @@ int sq_destroy(sq_ctx *c) {
     }
     if (c->frame_host) (void)hipHostFree(c->frame_host);
     (void)hipFree(c->ctl);
+    (void)hipFree(c->dstamps);
     (void)hipFree(c->rec_dev);
     (void)hipFree(c->fr_stable);
     (void)hipFree(c->fr_dtau);
@@ -1877,6 +1887,32 @@ int sq_step(sq_ctx *c, int nsteps) {
         c->region_steps += nsteps;
     }
     c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return SQ_OK;
+}
+
+int sq_phi4_block_stamps(sq_ctx *c, unsigned long long *out, int cap, int *nblocks) {
+    if (!c || !out || !nblocks || cap < 1) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (c->slabs.size() != 1 || c->p.comm != SQ_COMM_NONE || c->tbz <= 0)
+        return fail(SQ_E_STATE, "block stamps: one slab without an exchange, fused launches");
+    DeviceGuard g(c->dev);
+    const int need = std::max(cap, 4096);
+    if (c->stamps_cap < need) {
+        (void)hipFree(c->dstamps);
+        c->stamps_cap = 0;
+        SQ_HIP(hipMalloc(&c->dstamps, 2 * sizeof(unsigned long long) * (size_t)need));
+        c->stamps_cap = need;
+    }
+    c->stamps_next = c->dstamps;
+    c->stamps_blocks = 0;
+    int rc = phi4_steps(c, 2);
+    c->stamps_next = nullptr;
+    if (rc) return rc;
+    if (c->stamps_blocks > cap) return fail(SQ_E_ARG, "cap smaller than the launch's blocks");
+    SQ_HIP(hipMemcpyAsync(out, c->dstamps, 2 * sizeof(unsigned long long) * (size_t)c->stamps_blocks,
+                          hipMemcpyDeviceToHost, c->slabs[0].sA));
+    SQ_HIP(hipStreamSynchronize(c->slabs[0].sA));
+    *nblocks = c->stamps_blocks;
     return SQ_OK;
 }
 

@@ -66,6 +66,9 @@ struct Phi4StepArgs {
     // kernel of the previous frame may have changed Δτ)
     const float *dcoef;
     int prio;  // fused kernels: wave priority by march progress (prio_by_progress)
+    // fused kernels (nullable): per block b, the constant 100 MHz clock
+    // (s_memrealtime) at its start and end, stamps[2b], stamps[2b+1]
+    unsigned long long *stamps;
 };
 constexpr int kStabSlots = 32;
 

@@ -661,6 +661,13 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A0) {
 // gets the higher priority: 3 in its first quarter of planes, down to 0 in
 // its last (4 levels beat 2: 3 then 0 by halves, 512^3 139-140 vs 136-137
 // us/step).  q = quarter (0..3), wave-uniform.
+// Block stamps (Phi4StepArgs::stamps): the end, once every wave is done.
+__device__ __forceinline__ void block_end_stamp(const Phi4StepArgs &A) {
+    if (A.stamps == nullptr) return;
+    __syncthreads();
+    if (threadIdx.x == 0) A.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
 __device__ __forceinline__ void prio_by_progress(int q) {
     switch (q) {
     case 0: __builtin_amdgcn_s_setprio(3); break;
@@ -853,6 +860,7 @@ __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
+    if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
     // one XCD: the blocks sharing halo rows, edge columns and chunk-edge planes
     // meet in that XCD's L2
@@ -957,6 +965,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         frame_flush(A, f1, 0, sk, sa);
         frame_flush(A, f2, 1, sk, sa);
     }
+    block_end_stamp(A);
 }
 
 // ------------------------------------------- pipelined two-step fusion ----
@@ -1122,6 +1131,7 @@ __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A0) {
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
+    if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
     const int yb = lb % A.nyg, rest = lb / A.nyg;
     const int xs = WIDE ? rest % A.nxseg : 0, zk = WIDE ? rest / A.nxseg : rest;
@@ -1252,6 +1262,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
         frame_flush(A, f1, 0, sk, sa);
         frame_flush(A, f2, 1, sk, sa);
     }
+    block_end_stamp(A);
 }
 
 __global__ __launch_bounds__(256) void phi4_init_kernel(float *slab, int Lx, int Ly, int nz,

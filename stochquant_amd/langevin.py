@@ -307,6 +307,16 @@ class Phi4Lattice(_Ctx):
         _lib.call("sq_phi4_stability", self._h, _dptr(st), ctypes.byref(fired), _fptr(M), _fptr(D), _fptr(A), n)
         return {"T": st[0], "V": st[1], "fired": fired.value, "M": M, "D": D, "A": A}
 
+    def block_stamps(self, cap=1 << 16):
+        """Run 2 steps (one fused launch) with per-block clock stamps; returns
+        (start, end) int64 arrays in ticks of the 100 MHz constant clock."""
+        a = np.zeros(2 * cap, dtype=np.uint64)
+        nb = ctypes.c_int()
+        _lib.call("sq_phi4_block_stamps", self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), int(cap),
+                  ctypes.byref(nb))
+        a = a[:2 * nb.value].astype(np.int64)
+        return a[0::2], a[1::2]
+
     def set_stability(self, T, V):
         _lib.call("sq_phi4_set_stability", self._h, float(T), float(V))
 

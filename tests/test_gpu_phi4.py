@@ -905,3 +905,20 @@ def test_run_frames_after_upload_and_in_pieces(gpu, oracle_mod, monkeypatch):
     monkeypatch.setenv("SQ_FRAME_HOST", "1")
     c = run([30])
     assert np.array_equal(a[0], c[0]) and np.array_equal(a[1], c[1]) and np.array_equal(a[2], c[2])
+
+
+def test_block_stamps_are_two_steps(gpu, oracle_mod):
+    """sq_phi4_block_stamps runs exactly the next two steps (one fused launch)
+    and returns one start <= end stamp pair per block of that launch."""
+    shape = (256, 16, 24)
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    with _lat(shape) as L, _lat(shape) as R:
+        L.upload(phi0)
+        R.upload(phi0)
+        L.step(1)
+        R.step(1)
+        st, en = L.block_stamps()
+        R.step(2)
+        assert len(st) == len(en) > 0 and (en >= st).all() and (st > 0).all()
+        assert L.step_counter == R.step_counter == 3
+        assert np.array_equal(L.download(), R.download())
