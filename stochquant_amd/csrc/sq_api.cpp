@@ -1114,7 +1114,8 @@ int create_qm1d(sq_ctx *c) {
         SQ_HIP(hipMemset(c->qxx0[k], 0, bytes));
     }
     if (c->N > sq::kQm1dRegMaxN)  // global-memory variant: f ping-pong + scan scratch
-        for (double **q : {&c->qscr[0], &c->qscr[1], &c->qscr[2]}) SQ_HIP(hipMalloc(q, bytes));
+        for (int k = 0; k < 3; ++k)  // xs, ds: + the grid kernel's block maxima and scan words
+            SQ_HIP(hipMalloc(&c->qscr[k], k == 0 ? bytes : bytes + sizeof(double) * sq::kQm1dGridAux));
     SQ_HIP(hipMalloc(&c->qst, sizeof(sq::Qm1dState)));
     SQ_HIP(hipStreamCreateWithFlags(&c->qstream, hipStreamNonBlocking));
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream

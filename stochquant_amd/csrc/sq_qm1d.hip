@@ -17,6 +17,8 @@
 // scan partials go through LDS.  Expressions keep the reference's order and
 // the file is built with -ffp-contract=off, so for potID 0 the deterministic
 // part is bit-identical to the oracle.
+#include <hip/hip_cooperative_groups.h>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -498,6 +500,214 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
     }
 }
 
+// The same frame for N > 4096 on the whole chip (config C1's 32,768-site
+// chain; qm1d_frame_kernel_glob runs it on one CU): G = ceil(N / (256 K))
+// cooperative blocks of 256 threads, thread g owning sites [Kg, Kg+K) in
+// registers (drift checks and running means never leave them; K = 8).  ONE grid
+// barrier per step, between
+//   1. site updates from the old field (neighbours and f[mid] read from
+//      global memory, written by their owners before the last barrier),
+//      running means, guard, X' (parked in a by-parity buffer), drift check,
+//      per-block maxima of X' and |X'| (by parity);
+//   2. the outcome of the previous step's scan (its leader and instability:
+//      step-tagged atomic-max words its scan wrote before this barrier, so no
+//      slot needs resetting) -- an unstable previous step ends the frame here,
+//      this step's updates discarded as the one-CU kernel never makes them --
+//      then this step's ordered scan: every block forms the exclusive prefix
+//      over the blocks before it (G values) and the in-block prefix by wave
+//      scans, and walks its sites in order exactly as qm1d_frame_kernel_glob
+//      (a site is a leader when X' exceeds X'(E) and every X' before it,
+//      unstable when its drift check also exceeds V and every |X'| before it),
+//      then omega's step, computed redundantly by every thread.
+// Everything phase 2 of step j reads was written in phase 1 of step j (by
+// parity, so phase 1 of step j+1 in a faster block does not overwrite it) or
+// before the previous barrier.  Bit-identical to the one-CU kernel (same
+// expressions, the same order of every max; tests/test_gpu_qm1d.py::
+// test_grid_frame_equals_one_cu_frame, and the oracle tests at N > 4096).
+// Scratch: xs / ds (N + kGridAux doubles each) hold X' of even / odd steps,
+// xs[N..] the block maxima, ds[N..] the two tagged words.
+constexpr int kGridT = 256;
+
+template <int kGridK>
+__global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
+    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    __shared__ double s_wX[2][kGridT / 64], s_wA[2][kGridT / 64];
+    const int N = A.N, pot = A.pot, mid = N / 2, G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int gt = b * kGridT + t;
+    const int i0 = gt * kGridK;
+    const int own = max(0, min(kGridK, N - i0));
+    const double h = A.h, a = A.a, a2 = A.a2;
+    double *Xb[2] = {A.xs, A.ds};
+    double *bm = A.xs + N;  // [parity][X | A][G]
+    unsigned long long *lead = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lead + 1;
+    if (gt == 0) {
+        *lead = 0ull;
+        *unst = 0ull;
+    }
+    double nx[kGridK], nxx0[kGridK], D[kGridK];
+#pragma unroll
+    for (int k = 0; k < kGridK; ++k) {
+        nx[k] = k < own ? A.x[i0 + k] : 0.;
+        nxx0[k] = k < own ? A.xx0[i0 + k] : 0.;
+        D[k] = 0.;
+    }
+    double om = A.st->omega_in;
+    int E = A.st->lrgEl;
+    double V = A.st->lrgVl, totA = 0.;
+    int stable = 1, steps = 0;
+    const double *fin = A.f;
+    double *fout = A.nf;
+    for (int j = 0; j <= A.loops; ++j) {
+        const int par = j & 1;
+        double X[kGridK];
+        double ix = -INFINITY, ia = -INFINITY;
+        if (j < A.loops) {
+            // 1. site updates of step j
+            const unsigned long long step = A.tick + (unsigned long long)j;
+            const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
+            const double Xm = fin[mid] + xcl((double)mid * a, om, pot);
+            const double den = (double)(A.runs + j + 1);
+            double lmaxX = -INFINITY, lmaxA = -INFINITY;
+            if (own > 0) {
+                f32x4n nq = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
+                double fc[kGridK];
+#pragma unroll
+                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
+                const double fL = i0 > 0 ? fin[i0 - 1] : 0.;
+                const double fR = i0 + own < N ? fin[i0 + own] : 0.;
+#pragma unroll
+                for (int k = 0; k < kGridK; ++k) {
+                    if (k >= own) break;
+                    const int i = i0 + k;
+                    const int c = i & 3;  // component of site i's quad (K = 2: i0 may be 2 mod 4)
+                    if (c == 0 && k > 0)
+                        nq = normals4((unsigned long long)(i >> 2), kStreamField, slo, shi, A.k0, A.k1);
+                    const float xi = c == 0 ? nq.a : c == 1 ? nq.b : c == 2 ? nq.c : nq.d;
+                    const double fi = fc[k];
+                    const double fr = (k + 1 < own) ? fc[k + 1] : fR;
+                    const double prev_old = k == 0 ? fL : fc[k - 1];
+                    const double xc = xcl((double)i * a, om, pot);
+                    const double dw = A.sig * (double)xi;
+                    double v;
+                    if (i == 0)
+                        v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
+                            ddpot(xc, pot) * fi * h + dw;
+                    else if (i == N - 1)
+                        v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
+                            ddpot(xc, pot) * fi * h + dw;
+                    else
+                        v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
+                    if (v > 1000) v = 1000;
+                    if (v < -1000) v = -1000;
+                    if (v != v) v = 1000;
+                    X[k] = v + xc;
+                    D[k] = absol(v - fi - dw);
+                    lmaxX = fmax(lmaxX, X[k]);
+                    lmaxA = fmax(lmaxA, absol(X[k]));
+                    const double Xi = fi + xc;
+                    nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
+                    nx[k] = nx[k] + (Xi - nx[k]) / den;
+                    fout[i] = v;
+                    Xb[par][i] = X[k];
+                }
+            }
+            ix = wave_incl_max(lmaxX, lane);
+            ia = wave_incl_max(lmaxA, lane);
+            if (lane == 63) {
+                s_wX[par][wv] = ix;
+                s_wA[par][wv] = ia;
+            }
+            __syncthreads();
+            if (t == 0) {
+                double bx = -INFINITY, ba = -INFINITY;
+                for (int w = 0; w < kGridT / 64; ++w) {
+                    bx = fmax(bx, s_wX[par][w]);
+                    ba = fmax(ba, s_wA[par][w]);
+                }
+                bm[(2 * par) * G + b] = bx;
+                bm[(2 * par + 1) * G + b] = ba;
+            }
+        }
+        grid.sync();
+        __threadfence();
+        // 2a. the outcome of step j-1's scan
+        if (j > 0) {
+            const unsigned long long tag = (unsigned long long)j;
+            const unsigned long long lv = __hip_atomic_load(lead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((lv >> 32) == tag) E = (int)(lv & 0xffffffffull) - 1;
+            V = totA;
+            steps = j;
+            if (__hip_atomic_load(unst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == tag) {
+                stable = 0;
+                break;
+            }
+        }
+        if (j == A.loops) break;
+        // 2b. step j's ordered scan
+        double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
+        totA = V;
+        for (int q = 0; q < G; ++q) {
+            const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
+            if (q < b) {
+                runX = fmax(runX, qx);
+                runA = fmax(runA, qa);
+            }
+            totA = fmax(totA, qa);
+        }
+        for (int w = 0; w < wv; ++w) {
+            runX = fmax(runX, s_wX[par][w]);
+            runA = fmax(runA, s_wA[par][w]);
+        }
+        double ex = __shfl_up(ix, 1, 64), ea = __shfl_up(ia, 1, 64);
+        if (lane == 0) {
+            ex = -INFINITY;
+            ea = -INFINITY;
+        }
+        runX = fmax(runX, ex);
+        runA = fmax(runA, ea);
+        int un = 0, leader = -1;
+#pragma unroll
+        for (int k = 0; k < kGridK; ++k) {
+            if (k >= own) break;
+            if (X[k] > runX) {
+                runX = X[k];
+                leader = i0 + k;
+                if (D[k] > runA) un = 1;
+            }
+            runA = fmax(runA, absol(X[k]));
+        }
+        const unsigned long long tag1 = (unsigned long long)(j + 1);
+        if (leader >= 0) atomicMax(lead, (tag1 << 32) | (unsigned long long)(leader + 1));
+        if (un) atomicMax(unst, tag1);
+        // omega's step j
+        const unsigned long long step = A.tick + (unsigned long long)j;
+        const f32x4n nwn = normals4(0ull, kStreamOmega, (uint32_t)step, (uint32_t)(step >> 32), A.k0, A.k1);
+        const double nwo = om + A.kconst * (A.sigw * (double)nwn.a);
+        if (nwo > (double)(N - 1) * a) om = 2 * (double)(N - 1) * a - nwo;
+        else if (nwo < 0) om = -nwo;
+        else om = nwo;
+        fin = fout;
+        fout = (fout == A.nf) ? A.fs : A.nf;
+    }
+    // unstable after step s: the break came before iteration s+1's swap, so
+    // fin is step s's output, as in the one-CU kernel (the host discards it)
+#pragma unroll
+    for (int k = 0; k < kGridK; ++k) {
+        if (k >= own) break;
+        if (fin != A.nf) A.nf[i0 + k] = fin[i0 + k];
+        A.nx[i0 + k] = nx[k];
+        A.nxx0[i0 + k] = nxx0[k];
+    }
+    if (gt == 0) {
+        A.st->omega_out = om;
+        A.st->lrgEl = E;
+        A.st->lrgVl = V;
+        A.st->stable = stable;
+        A.st->steps_done = steps;
+    }
+}
+
 }  // namespace
 
 int qm1d_sites_per_thread(int N) {
@@ -555,6 +765,25 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         default: launch_wave<4>(a, W, s); break;
         }
         return hipGetLastError();
+    }
+    // N > 4096: the cooperative grid kernel (SQ_QM1D_GRID=0: the one-CU kernel)
+    const char *ge = getenv("SQ_QM1D_GRID");  // read per frame (tests switch it within a process)
+    const bool grid = ge ? atoi(ge) != 0 : true;
+    if (grid && a.N <= kQm1dMaxN) {
+        // sites per thread: 8 (N = 32,768: 16 blocks, 11.8 ms per 1000-step
+        // frame; 4: 14.2, 2: 22.6, 16: 18.6, 32: 51.3 -- profiles/r03/qm1d_grid/)
+        const char *gk = getenv("SQ_QM1D_GK");
+        const int kk = gk ? atoi(gk) : 8;
+        const int G = (a.N + kGridT * kk - 1) / (kGridT * kk);
+        if (4 * G > kQm1dGridAux) return hipErrorInvalidValue;  // xs[N..]: the block maxima by parity
+        Qm1dArgs q = a;
+        void *args[] = {&q};
+        const void *fn = kk == 2    ? (const void *)qm1d_frame_grid<2>
+                         : kk == 8  ? (const void *)qm1d_frame_grid<8>
+                         : kk == 16 ? (const void *)qm1d_frame_grid<16>
+                         : kk == 32 ? (const void *)qm1d_frame_grid<32>
+                                    : (const void *)qm1d_frame_grid<4>;
+        return hipLaunchCooperativeKernel(fn, dim3(G), dim3(kGridT), args, 0, s);
     }
     K = qm1d_sites_per_thread(a.N);
     if (K == 0) return hipErrorInvalidValue;

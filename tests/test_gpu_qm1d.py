@@ -201,3 +201,27 @@ def test_large_chain_double_well_within_tolerance(gpu, oracle_mod):
     tol = loops * (sig * 1.4e-5 + 2e-6)
     for k in ("f", "x", "xx0"):
         assert np.max(np.abs(d[k] - r[k])) <= tol
+
+
+@pytest.mark.parametrize("N,pot,C,h", [(8192, 3, 1.0, 0.002), (32768, 0, 1.0, 0.01), (65536, 3, 1.0, 0.002),
+                                       (4097, 0, 1.0, 0.002), (20000, 3, 1.0, 0.09)])
+def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h):
+    """N > 4096: the cooperative multi-block frame (qm1d_frame_grid, two grid
+    barriers per step) and the one-work-group frame (SQ_QM1D_GRID=0) are
+    bit-identical with the noise on: field, running means, omega, the carried
+    scan state and the verdict -- incl. a step size that makes the frame
+    unstable part-way (last case)."""
+    a, loops = 0.1, 40
+    f, x, xx0 = _state(N, seed=11, amp=0.3)
+    om = N * a / 2 + 0.013
+
+    def run(grid):
+        monkeypatch.setenv("SQ_QM1D_GRID", grid)
+        return _gpu_frame(N, a, h, pot, C, loops, 5, f, x, xx0, om, runs=3, lrgEl=N // 3, lrgVl=0.2, tick=11)
+
+    s1, d1, c1 = run("1")
+    s0, d0, c0 = run("0")
+    assert s1 == s0
+    for k in ("f", "x", "xx0"):
+        assert np.array_equal(d1[k], d0[k]), k
+    assert d1["omega"] == d0["omega"] and c1 == c0
