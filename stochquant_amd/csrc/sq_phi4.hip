@@ -668,6 +668,17 @@ __device__ __forceinline__ void block_end_stamp(const Phi4StepArgs &A) {
     if (threadIdx.x == 0) A.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
+// The march's quarter boundaries: plane p (p = z0-1 .. z1) is in quarter
+// floor(4 (p - z0 + 1) / span) = (p >= t[0]) + (p >= t[1]) + (p >= t[2]),
+// t[k] = z0 - 1 + ceil((k+1) span / 4) -- three compares per iteration instead
+// of a signed division.
+struct PrioQ {
+    int t0, t1, t2;
+    __device__ __forceinline__ PrioQ(int z0, int span)
+        : t0(z0 - 1 + (span + 3) / 4), t1(z0 - 1 + (2 * span + 3) / 4), t2(z0 - 1 + (3 * span + 3) / 4) {}
+    __device__ __forceinline__ int q(int p) const { return (p >= t0) + (p >= t1) + (p >= t2); }
+};
+
 __device__ __forceinline__ void prio_by_progress(int q) {
     switch (q) {
     case 0: __builtin_amdgcn_s_setprio(3); break;
@@ -950,9 +961,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
     R.qzm = 0;  // plane z0-2: no step s+1 output there
     // three-plane queues unrolled three ways so no rotation moves are emitted
-    const int span = z1 - K.z0 + 2;
+    const PrioQ pq(K.z0, z1 - K.z0 + 2);
     for (int p = K.z0 - 1; p <= z1; p += 3) {
-        if (A.prio) prio_by_progress(4 * (p - K.z0 + 1) / span);
+        if (A.prio) prio_by_progress(pq.q(p));
         tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2, bmx);
         if (p + 1 > z1) break;
         tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2, bmx);
@@ -1225,9 +1236,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
         if (xrow) in_lds[0][xslot][K.lane] = X[0];
         T[0] = T[1] = T[2] = T[3] = make_float4(0.f, 0.f, 0.f, 0.f);
         __syncthreads();
-        const int span = z1 - K.z0 + 2;
+        const PrioQ pq(K.z0, z1 - K.z0 + 2);
         for (int k = K.z0 - 1; k <= z1; k += 4) {
-            if (A.prio) prio_by_progress(4 * (k - K.z0 + 1) / span);
+            if (A.prio) prio_by_progress(pq.q(k));
             tp_row<NZ, WIDE, FR, WH, 0>(A, K, R, k, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
             if (k + 1 > z1) break;
             tp_row<NZ, WIDE, FR, WH, 1>(A, K, R, k + 1, xrow, vxr, xslot, I, T, X, E, in_lds, t_lds, tx, f1, f2, bmx);
@@ -1244,9 +1255,9 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
         C[2] = bload1(p2, K.voff);
         NB[0] = make_float4(bload1(p1, K.vex), bload1(p1, K.vx2), bload1(p1, K.vm), bload1(p1, K.vp));
         __syncthreads();
-        const int span = z1 - K.z0 + 2;
+        const PrioQ pq(K.z0, z1 - K.z0 + 2);
         for (int k = K.z0 - 1; k <= z1; k += 4) {
-            if (A.prio) prio_by_progress(4 * (k - K.z0 + 1) / span);
+            if (A.prio) prio_by_progress(pq.q(k));
             tp_xhalo<NZ, WH, 0>(A, K, R, k, C, NB, tx);
             if (k + 1 > z1) break;
             tp_xhalo<NZ, WH, 1>(A, K, R, k + 1, C, NB, tx);
