@@ -880,6 +880,13 @@ int phi4_join(sq_ctx *c) {
     return SQ_OK;
 }
 
+// Before an observable's kernels on stream A: one slab without an exchange
+// puts every step on stream A, so stream order suffices; otherwise join.
+int observe_join(sq_ctx *c) {
+    if (c->slabs.size() == 1 && c->p.comm == SQ_COMM_NONE) return SQ_OK;
+    return phi4_join(c);
+}
+
 // Point st_md / st_a / flag at record set k of frame_rec (st_md | st_a | flag).
 void use_rec_set(sq_ctx *c, int k) {
     const size_t nrec = (size_t)sq::kStabSlots * (size_t)std::max(c->p.loops, 0);
@@ -2108,7 +2115,7 @@ int sq_moments(sq_ctx *c, double out[3]) {
     if (!c || !out) return fail(SQ_E_ARG, "null argument");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
     DeviceGuard g(c->dev);
-    int rc = phi4_join(c);
+    int rc = observe_join(c);
     if (rc) return rc;
     const size_t plane = plane_floats(c);
     out[0] = out[1] = out[2] = 0;
@@ -2174,7 +2181,7 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     if (n > c->Lz) return fail(SQ_E_ARG, "n > Lz");
     if (c->p.comm == SQ_COMM_P2P && !c->p2p_ready)
         return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
-    int rc = phi4_join(c);
+    int rc = observe_join(c);
     if (rc) return rc;
     // slice sums S(z) of the whole lattice: every slab writes its planes into a
     // zeroed global-length array; across ranks one RCCL sum all-reduce (the
@@ -2185,10 +2192,10 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     double *d = c->dslice;
     hipStream_t s0 = c->slabs[0].sA;
     hipError_t e = hipMemsetAsync(d, 0, sizeof(double) * (size_t)Lz, s0);
-    for (auto &s : c->slabs) {
-        if (e == hipSuccess) e = hipStreamSynchronize(s0);
+    for (auto &s : c->slabs) {  // one slab: stream order alone, one synchronisation below
+        if (e == hipSuccess && s.sA != s0) e = hipStreamSynchronize(s0);
         if (e == hipSuccess) e = sq::phi4_slices_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, d + s.z0, s.sA);
-        if (e == hipSuccess) e = hipStreamSynchronize(s.sA);
+        if (e == hipSuccess && s.sA != s0) e = hipStreamSynchronize(s.sA);
     }
     if (e == hipSuccess && per_rank(c->p.comm) && c->p.nranks > 1) {
         // disjoint z ranges, zeros elsewhere: the sum is exact in any order
@@ -2198,9 +2205,10 @@ int sq_correlator(sq_ctx *c, double *out, int n) {
     if (e == hipSuccess) e = hipStreamSynchronize(s0);
     if (e != hipSuccess) return fail(SQ_E_HIP, hipGetErrorString(e));
     const double vol = (double)c->Lx * c->Ly * (double)Lz;
-    for (int t = 0; t < n; ++t) {
+    for (int t = 0; t < n; ++t) {  // z ascending, the wrap without a modulo per term
         double acc = 0;
-        for (long long z = 0; z < Lz; ++z) acc += S[z] * S[(z + t) % Lz];
+        for (long long z = 0; z < Lz - t; ++z) acc += S[z] * S[z + t];
+        for (long long z = Lz - t; z < Lz; ++z) acc += S[z] * S[z + t - Lz];
         out[t] = acc / vol;
     }
     return SQ_OK;
