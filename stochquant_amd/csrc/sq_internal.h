@@ -192,6 +192,7 @@ struct Qm1dArgs {
     double a, a2, h, sig, sigw, kconst;
     uint32_t k0, k1;
     unsigned long long tick;    // Philox step index of the frame's first step
+    int gbar;                   // qm1d_frame_grid: 1 = its own counter barrier (else cooperative groups)
 };
 
 int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant: N > kQm1dRegMaxN)

@@ -528,9 +528,25 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
 // xs[N..] the block maxima, ds[N..] the two tagged words.
 constexpr int kGridT = 256;
 
+// Grid barrier of a cooperative launch (all blocks co-resident): thread 0 of
+// each block releases its block's writes, counts the block in and spins until
+// every block of barrier `n` (1-based) has; the counter was zeroed ahead of the
+// launch.  A vector atomic and a relaxed load, no scalar-memory writes.
+__device__ __forceinline__ void grid_barrier(unsigned int *ctr, unsigned int n) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int target = n * gridDim.x;
+        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target)
+            __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+}
+
 template <int kGridK>
 __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    unsigned int *bar = reinterpret_cast<unsigned int *>(A.ds + A.N) + 4;  // zeroed before the launch
     __shared__ double s_wX[2][kGridT / 64], s_wA[2][kGridT / 64];
     const int N = A.N, pot = A.pot, mid = N / 2, G = (int)gridDim.x, b = (int)blockIdx.x;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -629,7 +645,10 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                 bm[(2 * par + 1) * G + b] = ba;
             }
         }
-        grid.sync();
+        if (A.gbar)
+            grid_barrier(bar, (unsigned int)(j + 1));
+        else
+            grid.sync();
         __threadfence();
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
@@ -777,6 +796,14 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         const int G = (a.N + kGridT * kk - 1) / (kGridT * kk);
         if (4 * G > kQm1dGridAux) return hipErrorInvalidValue;  // xs[N..]: the block maxima by parity
         Qm1dArgs q = a;
+        // the counter barrier: N = 32,768 10.8 vs 11.7 ms per 1000-step frame with
+        // cooperative groups' grid.sync (profiles/r03/qm1d_grid/); SQ_QM1D_BAR=0
+        const char *gb = getenv("SQ_QM1D_BAR");
+        q.gbar = gb ? atoi(gb) : 1;
+        if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (after the tagged words)
+            hipError_t e = hipMemsetAsync(reinterpret_cast<unsigned int *>(q.ds + q.N) + 4, 0, sizeof(unsigned int), s);
+            if (e != hipSuccess) return e;
+        }
         void *args[] = {&q};
         const void *fn = kk == 2    ? (const void *)qm1d_frame_grid<2>
                          : kk == 8  ? (const void *)qm1d_frame_grid<8>
