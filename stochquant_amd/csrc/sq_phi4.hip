@@ -243,9 +243,15 @@ __device__ __forceinline__ void frame_sites(const Phi4StepArgs &A, FrameAcc &f, 
     f.am = vmax(f.am, mo);  // mo: never a signalling NaN (arithmetic / the guard's output)
     {  // frame launches always carry the records (the launchers check st_md, st_a)
         const float o4 = vmax(vmax3(o.x, o.y, o.z), o.w);  // the guard's output: never NaN
-        float t = f.mw;
-        if constexpr (BW) t = vmax(t, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (__ballot(o4 >= t) != 0ull) {
+        if (__ballot(o4 >= f.mw) == 0ull) return;  // below the wave's own threshold: no LDS read
+        if constexpr (BW) {
+            // the block's threshold only when the wave's own one is met; it becomes
+            // the wave's (any attained value <= the record's maximum is exact, and
+            // the block word only grows), so the next float4s test against it
+            // without another LDS read
+            f.mw = vmax(f.mw, __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        }
+        if (!BW || __ballot(o4 >= f.mw) != 0ull) {
             const float s = NZ ? A.sigq : 0.f;
             stab_site(f, o.x, c.x, xi.a, s);
             stab_site(f, o.y, c.y, xi.b, s);
