@@ -1,7 +1,7 @@
 """Build libstochquant.so with a patched copy of one device source, for A/B runs
 (SQ_LIB=<path> selects it at load time).
 
-    python scripts/build_variant.py <patched sq_phi4.hip> <name>
+    python scripts/build_variant.py <patched source> <name> [replaced source, default sq_phi4.hip]
       -> stochquant_amd/lib/variants/libstochquant_<name>.so
 """
 import os
@@ -16,19 +16,21 @@ from stochquant_amd import build  # noqa: E402
 
 def main():
     src, name = sys.argv[1], sys.argv[2]
+    which = sys.argv[3] if len(sys.argv) > 3 else "sq_phi4.hip"
+    assert which in build.DEVICE_SOURCES, which
     build.build()
     tmp = os.path.join(ROOT, "stochquant_amd", "_obj", "variants", name)
     os.makedirs(tmp, exist_ok=True)
     dst_src = os.path.join(build.CSRC, "_variant_" + name + ".hip")
     shutil.copy(src, dst_src)
     try:
-        obj = os.path.join(tmp, "sq_phi4.hip.o")
+        obj = os.path.join(tmp, which + ".o")
         subprocess.run([build.HIPCC] + build.COMMON + [f"--offload-arch={build.ARCH}", "-x", "hip", "-c", dst_src,
                         "-o", obj], check=True)
     finally:
         os.remove(dst_src)
     objs = [obj] + [os.path.join(build.OBJ, s + ".o") for s in build.DEVICE_SOURCES + build.HOST_SOURCES
-                    if s != "sq_phi4.hip"]
+                    if s != which]
     out = os.path.join(build.LIBDIR, "variants", f"libstochquant_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     subprocess.run([build.HIPCC, f"--offload-arch={build.ARCH}", "-shared", "-fPIC", "-o", out] + objs

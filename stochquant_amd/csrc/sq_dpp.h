@@ -21,15 +21,34 @@ template <int CTRL, int RM, int BM>
 __device__ __forceinline__ int dpp_i(int v, int id) {
     return __builtin_amdgcn_update_dpp(id, v, CTRL, RM, BM, false);
 }
+// v_max_f64 as is: fmax of a DPP-moved value (integer moves to the compiler)
+// gets a quieting v_max_f64 x, x, x per operand first; the scanned values are
+// results of arithmetic, never signalling NaNs, and a quiet NaN still yields
+// the other operand
+__device__ __forceinline__ double dpp_vmax_d(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// A lane with no source lane (or a row the mask leaves out) keeps the moved
+// register's previous contents instead of a fresh -inf: that register only
+// ever holds -inf or a value moved from a lower lane, which the inclusive
+// maximum already covers, so the scan is unchanged and the two moves of the
+// identity per stage go away.
 __device__ __forceinline__ double dpp_incl_max(double v) {
-    const double id = -__builtin_inf();
-    v = fmax(v, dpp_d<0x111, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x112, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x114, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x118, 0xf, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x142, 0xa, 0xf>(v, id));
-    v = fmax(v, dpp_d<0x143, 0xc, 0xf>(v, id));
-    return v;
+    double t = -__builtin_inf();
+    t = dpp_d<0x111, 0xf, 0xf>(v, t);
+    v = dpp_vmax_d(v, t);
+    t = dpp_d<0x112, 0xf, 0xf>(v, t);
+    v = dpp_vmax_d(v, t);
+    t = dpp_d<0x114, 0xf, 0xf>(v, t);
+    v = dpp_vmax_d(v, t);
+    t = dpp_d<0x118, 0xf, 0xf>(v, t);
+    v = dpp_vmax_d(v, t);
+    t = dpp_d<0x142, 0xa, 0xf>(v, t);
+    v = dpp_vmax_d(v, t);
+    t = dpp_d<0x143, 0xc, 0xf>(v, t);
+    return dpp_vmax_d(v, t);
 }
 __device__ __forceinline__ double dpp_excl_max(double v) {  // max over lanes < this lane
     return dpp_d<0x138, 0xf, 0xf>(dpp_incl_max(v), -__builtin_inf());  // wave_shr:1

@@ -54,6 +54,49 @@ __device__ __forceinline__ float xcl_tanh(double t, double w) {
     return sq_glibc_tanhf((float)(s * (t - w) / kEta));
 }
 
+// a / b for a divisor b shared by many quotients (a2 for the frame, the step's
+// den), bit-identical to the compiler's fp64 division.  That expansion is
+//   r = rcp(b'); two Newton steps R = fma(r1, fma(-b', r1, 1), r1) with
+//   r1 = fma(r, fma(-b', r, 1), r); m = a' R; q = fixup(fmas(fma(-b', m, a'), R, m))
+// where b', a' are v_div_scale's operands: b and a themselves, with vcc clear,
+// unless an exponent is extreme.  With b in [2^-60, 2^60] (UDiv::ok) and
+// 2^-960 < |a| < 2^700 nothing is scaled, div_fmas is a plain fma and
+// div_fixup returns its (finite, normal) input, so R is computed once per
+// divisor and a quotient is a multiply and two fmas instead of 10 instructions
+// with a quarter-rate v_rcp_f64.  Any other a (0, -0, inf, NaN, tiny or huge)
+// takes the full division (udiv_step).
+struct UDiv {
+    double b, r;
+    bool ok;  // b in [2^-60, 2^60]: otherwise every quotient takes the full division
+};
+__device__ __forceinline__ UDiv udiv_prep(double b) {
+    const double r0 = __builtin_amdgcn_rcp(b);
+    const double r1 = __builtin_fma(r0, __builtin_fma(-b, r0, 1.0), r0);
+    return UDiv{b, __builtin_fma(r1, __builtin_fma(-b, r1, 1.0), r1), b >= 0x1p-60 && b <= 0x1p+60};
+}
+__device__ __forceinline__ bool udiv_range(double a) {  // false for 0, NaN, inf, tiny, huge
+    const double x = __builtin_fabs(a);
+    return x > 0x1p-960 && x < 0x1p+700;
+}
+__device__ __forceinline__ double udiv_fast(double a, const UDiv &d) {
+    const double m = a * d.r;
+    return __builtin_fma(__builtin_fma(-d.b, m, a), d.r, m);
+}
+// The quotients of one step: the fast form unless some lane of the wave has a
+// numerator outside its range (one wave-uniform branch per step, not one per
+// quotient: per-quotient branches cost more than the division they skip).
+template <int M, bool FAST>
+__device__ __forceinline__ void udiv_step(const double (&n)[M], const UDiv &d, double (&q)[M], bool bad) {
+    if (!FAST || __ballot(bad || !d.ok) != 0ull) {
+        asm volatile("");  // a real branch: an fdiv is one IR instruction, cheap enough to speculate
+#pragma unroll
+        for (int k = 0; k < M; ++k) q[k] = n[k] / d.b;
+    } else {
+#pragma unroll
+        for (int k = 0; k < M; ++k) q[k] = udiv_fast(n[k], d);
+    }
+}
+
 __device__ __forceinline__ double wave_incl_max(double v, int lane) {
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -116,19 +159,24 @@ __device__ __forceinline__ void load_tab(const Qm1dArgs &A, int j, int i0, int m
     }
 }
 
-template <int K, bool MW>
+template <int K, bool MW, bool P3>
 __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs A) {
     constexpr int kW = 16;
     __shared__ double s_first[2][kW], s_last[2][kW], s_mx[2][kW], s_ma[2][kW];
     __shared__ int s_arg[2][kW], s_un[2][kW];
     __shared__ double s_fmid[2], s_xe[2];
 
-    const int N = A.N, pot = A.pot, mid = N / 2;
-    const bool p3 = pot == 3;
+    const int N = A.N, mid = N / 2;
+    constexpr bool p3 = P3;  // potID 3 (the launcher picks the instance by A.pot)
+    // the shared-divisor division pays at 4 sites per lane (N = 1000: 3.12 -> 2.71 ms
+    // per 1000-step frame, N = 3072: 1.20 -> 0.95); with fewer sites the step's
+    // uniform branch costs more than it saves (N = 100: 1.18 -> 1.24)
+    constexpr bool kFastDiv = K >= 4;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int W = MW ? (int)(blockDim.x >> 6) : 1;
     const int i0 = (int)threadIdx.x * K;
-    const double h = A.h, a2 = A.a2;
+    const double h = A.h;
+    const UDiv da2 = udiv_prep(A.a2);
     const double ninf = -__builtin_inf();
 
     double f[K], x[K], xx0[K], Xn[K], dchk[K];
@@ -164,8 +212,35 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
         if (j + 1 < A.loops) load_tab<K>(A, j + 1, i0, mid, p3, nxt);  // one step ahead
         // ---- 1. site updates ----
         const double Xm = fmid + (p3 ? kEta * (double)cur.tm : 0.);
-        const double den = (double)(A.runs + j + 1);
-        double prev_old = fL;  // old f[i-1]
+        const UDiv dden = udiv_prep((double)(A.runs + j + 1));
+        // numerators first, then every quotient of the step (udiv_step)
+        double nA[K], qA[K];
+        double nM2[2 * K], qM2[2 * K];  // the running means': xx0's K numerators, then x's
+        bool bad = false;
+        {
+            double prev_old = fL;  // old f[i-1]
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = i0 + k;
+                const double fi = f[k];
+                const double xc = p3 ? kEta * (double)cur.t[k] : 0.;  // clas(), :184-189
+                const double fr = (k + 1 < K) ? f[k + 1] : fR;
+                if (i == 0)
+                    nA[k] = kM * h * (fr + (-kEta) - (p3 ? kEta * (double)cur.tl : 0.) - 2 * fi);
+                else if (i == N - 1)
+                    nA[k] = kM * h * (prev_old + kEta - (p3 ? kEta * (double)cur.tr : 0.) - 2 * fi);
+                else
+                    nA[k] = kM * h * (fr + prev_old - 2 * fi);
+                // running means from the OLD field, :144-145
+                const double Xi = fi + xc;
+                nM2[k] = Xi * Xm - xx0[k];
+                nM2[K + k] = Xi - x[k];
+                if (i < N) bad = bad || !(udiv_range(nA[k]) && udiv_range(nM2[k]) && udiv_range(nM2[K + k]));
+                prev_old = fi;
+            }
+        }
+        udiv_step<K, kFastDiv>(nA, da2, qA, bad);
+        udiv_step<2 * K, kFastDiv>(nM2, dden, qM2, bad);
         double lmaxX = ninf, lmaxA = ninf;
         int larg = 0;
 #pragma unroll
@@ -178,16 +253,7 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
                 const double xc = p3 ? kEta * (double)cur.t[k] : 0.;  // clas(), :184-189
                 const double dp = p3 ? cur.dd[k] : 2.;                // ddPot(), :190-195
                 const double dw = A.sig * (double)cur.xi[k];
-                const double fr = (k + 1 < K) ? f[k + 1] : fR;
-                double v;
-                if (i == 0)
-                    v = fi + kM * h * (fr + (-kEta) - (p3 ? kEta * (double)cur.tl : 0.) - 2 * fi) / a2 -
-                        dp * fi * h + dw;
-                else if (i == N - 1)
-                    v = fi + kM * h * (prev_old + kEta - (p3 ? kEta * (double)cur.tr : 0.) - 2 * fi) / a2 -
-                        dp * fi * h + dw;
-                else
-                    v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - dp * fi * h + dw;
+                double v = fi + qA[k] - dp * fi * h + dw;
                 if (v > 1000) v = 1000;  // guard, :119-133
                 if (v < -1000) v = -1000;
                 if (v != v) v = 1000;
@@ -199,11 +265,8 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
                     larg = i;
                 }
                 lmaxA = fmax(lmaxA, absol(X));
-                // running means from the OLD field, :144-145
-                const double Xi = fi + xc;
-                xx0[k] = xx0[k] + (Xi * Xm - xx0[k]) / den;
-                x[k] = x[k] + (Xi - x[k]) / den;
-                prev_old = fi;
+                xx0[k] = xx0[k] + qM2[k];
+                x[k] = x[k] + qM2[K + k];
                 f[k] = v;
             }
         }
@@ -761,10 +824,15 @@ static bool qm1d_wave_shape(int N, int &K, int &W) {
     return K <= 4;
 }
 
+template <int K, bool P3>
+static void launch_wave_p(const Qm1dArgs &a, int W, hipStream_t s) {
+    if (W == 1) hipLaunchKernelGGL((qm1d_frame_wave<K, false, P3>), dim3(1), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((qm1d_frame_wave<K, true, P3>), dim3(1), dim3(64 * W), 0, s, a);
+}
 template <int K>
 static void launch_wave(const Qm1dArgs &a, int W, hipStream_t s) {
-    if (W == 1) hipLaunchKernelGGL((qm1d_frame_wave<K, false>), dim3(1), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((qm1d_frame_wave<K, true>), dim3(1), dim3(64 * W), 0, s, a);
+    if (a.pot == 3) launch_wave_p<K, true>(a, W, s);
+    else launch_wave_p<K, false>(a, W, s);
 }
 
 hipError_t qm1d_prep_launch(const Qm1dArgs &a, hipStream_t s) {
