@@ -131,7 +131,9 @@ __device__ __forceinline__ double pick(const double (&v)[K], int k) {  // v[k], 
 //      before it and X'(E) while its drift check exceeds V and every |X'|
 //      before it (oracle/orc_qm1d.c orc_qm1d_frame, tau_kernel.cl:135-143).
 // One wave needs no barrier at all (readlane / ballot); W waves use two per
-// step, with the LDS slots double-buffered by step parity.
+// step, with the LDS slots double-buffered by step parity.  The maxima are
+// v_max_f64 as is (dpp_vmax_d): every operand is a result of arithmetic or
+// the carried state, never a signalling NaN, so fmax's quieting is dead weight.
 template <int K>
 struct StepTab {  // one step's table values of a lane's K sites
     float xi[K], t[K];
@@ -207,7 +209,9 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
     StepTab<K> cur, nxt;
     load_tab<K>(A, 0, i0, mid, p3, cur);
 
-    for (int j = 0; j < A.loops; ++j) {
+    // one step; true when it ends the frame.  Unrolled two ways below so the
+    // tables alternate between cur and nxt without copies.
+    auto step = [&](const int j, const StepTab<K> &cur, StepTab<K> &nxt) -> bool {
         const int p = j & 1;
         if (j + 1 < A.loops) load_tab<K>(A, j + 1, i0, mid, p3, nxt);  // one step ahead
         // ---- 1. site updates ----
@@ -264,7 +268,7 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
                     lmaxX = X;
                     larg = i;
                 }
-                lmaxA = fmax(lmaxA, absol(X));
+                lmaxA = dpp_vmax_d(lmaxA, absol(X));
                 xx0[k] = xx0[k] + qM2[k];
                 x[k] = x[k] + qM2[K + k];
                 f[k] = v;
@@ -296,10 +300,10 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
             for (int w = 0; w < W; ++w) {
                 const double mx = s_mx[p][w], ma = s_ma[p][w];
                 if (w < wv) {
-                    pX = fmax(pX, mx);
-                    pA = fmax(pA, ma);
+                    pX = dpp_vmax_d(pX, mx);
+                    pA = dpp_vmax_d(pA, ma);
                 }
-                totA = fmax(totA, ma);
+                totA = dpp_vmax_d(totA, ma);
                 if (mx > gX) {
                     gX = mx;
                     garg = s_arg[p][w];
@@ -311,9 +315,9 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
             pA = V;
             gX = wmx;
             garg = warg;
-            totA = fmax(V, wma);
+            totA = dpp_vmax_d(V, wma);
         }
-        double runX = fmax(pX, dpp_excl_max(lmaxX)), runA = fmax(pA, dpp_excl_max(lmaxA));
+        double runX = dpp_vmax_d(pX, dpp_excl_max(lmaxX)), runA = dpp_vmax_d(pA, dpp_excl_max(lmaxA));
         int unst = 0;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -321,7 +325,7 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
                 runX = Xn[k];
                 if (dchk[k] > runA) unst = 1;
             }
-            runA = fmax(runA, absol(Xn[k]));
+            runA = dpp_vmax_d(runA, absol(Xn[k]));
         }
         int any = __ballot(unst) != 0ull;
         // neighbours of the new field for the next step
@@ -343,9 +347,13 @@ __global__ __launch_bounds__(MW ? 1024 : 64) void qm1d_frame_wave(const Qm1dArgs
         steps = j + 1;
         if (any) {
             stable = 0;
-            break;
+            return true;
         }
-        cur = nxt;
+        return false;
+    };
+    for (int j = 0; j < A.loops; j += 2) {
+        if (step(j, cur, nxt)) break;
+        if (j + 1 >= A.loops || step(j + 1, nxt, cur)) break;
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
