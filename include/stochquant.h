@@ -191,6 +191,11 @@ int sq_phi4_ghost(sq_ctx *ctx, int *active, int *allocated);
  * and whether the timed trials chose them (1) or they are the defaults /
  * SQ_CORE_PAIRS / SQ_RIMS_B (0).  Single periodic slab: 0, 0, 0. */
 int sq_phi4_schedule(sq_ctx *ctx, int *core_pairs, int *rims_b, int *tuned);
+/* Whether the block's last pair computes the slab's edge planes first, so the
+ * next exchange starts before the middle (1), or runs whole (0).  Default: 1,
+ * except 0 for one rank's RCCL self-exchange; the timed trials of multi-rank
+ * contexts try both; SQ_EDGE_FIRST=0|1 pins it.  Single periodic slab: 0. */
+int sq_phi4_edge_first(sq_ctx *ctx, int *edge_first);
 /* The launch schedule of one deep-halo block (pure host logic, no device
  * needed; the product's phi4_block executes exactly this list): a slab of nz
  * planes with a ghost zone of `ghost` planes (the exchange depth G) running

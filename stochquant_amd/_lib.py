@@ -113,6 +113,7 @@ SIGNATURES = {
     "sq_phi4_kernel": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
     "sq_phi4_ghost": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "sq_phi4_schedule": (ctypes.c_int, [_P, _I, _I, _I]),
+    "sq_phi4_edge_first": (ctypes.c_int, [_P, _I]),
     "sq_phi4_block_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
     "sq_phi4_pick_ghost": (ctypes.c_int, [_D, ctypes.c_int]),

@@ -181,7 +181,8 @@ struct sq_ctx {
                                // came from sq_init_field); false after a caller's upload / load
     bool fin_sync = false;     // multi-rank: field_finite changed locally; the next step call
                                // agrees on it across ranks first (ghost planes come from neighbours)
-    bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0: off)
+    bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0|1 pins it)
+    bool ef_auto = true;    // the timed pick also tries the other edge_first (unless SQ_EDGE_FIRST pins it)
     int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
     bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
                             // (SQ_CORE_PAIRS pins; multi-rank runs time 1, 2, 4 on the real link)
@@ -755,19 +756,25 @@ int phi4_join(sq_ctx *c);
 int phi4_autotune(sq_ctx *c, int &n) {
     struct Cand {
         int g, k;
-        bool rb;
+        bool rb, ef;
     };
     std::vector<Cand> cand;
+    const bool ef = c->edge_first;
     for (int g : {4, 8, 16})
-        if (g <= c->gpad) cand.push_back({g, c->core_pairs, c->rims_b});
-    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs, c->rims_b});
+        if (g <= c->gpad) cand.push_back({g, c->core_pairs, c->rims_b, ef});
+    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs, c->rims_b, ef});
+    const int gd = cand.back().g;
     if (c->tbz > 0 && c->k_auto) {
-        const int gd = cand.back().g;
-        cand.push_back({gd, 0, false});
+        cand.push_back({gd, 0, false, ef});
         for (bool rb : {false, true})
             for (int k : {2, 4})
-                if (k <= gd / 2) cand.push_back({gd, k, rb});
+                if (k <= gd / 2) cand.push_back({gd, k, rb, ef});
     }
+    // the edges-first split of the block's last pair buys the next exchange a
+    // longer window at the price of a split launch and an event bubble: worth
+    // it when the exchange is long (a real link), not on one GPU (19.3 vs 19.9
+    // us/step at 256^3, profiles/r03/s2/slab_ef/), so both are timed
+    if (c->ef_auto) cand.push_back({gd, c->core_pairs, c->rims_b, !ef});
     if (cand.size() > 16) cand.resize(16);  // dtune holds 16 times
     int need = 0;
     for (const Cand &k : cand) need += 3 * k.g;
@@ -781,6 +788,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
         c->gz = g;
         c->core_pairs = cand[k].k;
         c->rims_b = cand[k].rb;
+        c->edge_first = cand[k].ef;
         int rc = phi4_block(c, g);
         if (!rc) rc = phi4_join(c);
         if (rc) return rc;
@@ -810,6 +818,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
     c->gz = best.g;
     c->core_pairs = best.k;
     c->rims_b = best.rb;
+    c->edge_first = best.ef;
     c->g_tuned = true;
     return SQ_OK;
 }
@@ -1059,7 +1068,16 @@ int create_phi4(sq_ctx *c) {
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     while (zc < 32 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 32768) zc *= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
-    if (const char *e = getenv("SQ_EDGE_FIRST")) c->edge_first = atoi(e) != 0;
+    // edges-first by default except for one rank's RCCL self-exchange, which is
+    // short enough to fit beside the next core pair (off: 19.2-19.4 vs 19.9
+    // us/step; the P2P self-exchange's flag round trips want the early start:
+    // 20.9-21.1 off vs 20.2-20.4 on); the timed pick of multi-rank contexts
+    // tries both
+    c->edge_first = !(c->p.comm == SQ_COMM_RCCL && c->p.nranks == 1);
+    if (const char *e = getenv("SQ_EDGE_FIRST")) {
+        c->edge_first = atoi(e) != 0;
+        c->ef_auto = false;
+    }
     if (const char *e = getenv("SQ_CORE_PAIRS")) {
         c->core_pairs = std::max(0, atoi(e));
         c->k_auto = false;
@@ -1985,6 +2003,13 @@ int sq_phi4_schedule(sq_ctx *c, int *core_pairs, int *rims_b, int *tuned) {
     if (core_pairs) *core_pairs = slab ? c->core_pairs : 0;
     if (rims_b) *rims_b = slab && c->rims_b ? 1 : 0;
     if (tuned) *tuned = c->g_tuned ? 1 : 0;
+    return SQ_OK;
+}
+
+int sq_phi4_edge_first(sq_ctx *c, int *edge_first) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (edge_first) *edge_first = c->p.comm != SQ_COMM_NONE && c->edge_first ? 1 : 0;
     return SQ_OK;
 }
 

@@ -284,10 +284,12 @@ class Phi4Lattice(_Ctx):
 
     @property
     def schedule(self):
-        """{"ghost", "core_pairs", "rims_b", "tuned"} of a slab decomposition's block schedule."""
-        k, b, t = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        """{"ghost", "core_pairs", "rims_b", "edge_first", "tuned"} of a slab decomposition's block schedule."""
+        k, b, t, e = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.call("sq_phi4_schedule", self._h, ctypes.byref(k), ctypes.byref(b), ctypes.byref(t))
-        return {"ghost": self.ghost[0], "core_pairs": k.value, "rims_b": bool(b.value), "tuned": bool(t.value)}
+        _lib.call("sq_phi4_edge_first", self._h, ctypes.byref(e))
+        return {"ghost": self.ghost[0], "core_pairs": k.value, "rims_b": bool(b.value), "edge_first": bool(e.value),
+                "tuned": bool(t.value)}
 
     def save(self, path):
         """Binary checkpoint: <path> (.npy float32 (nz, Ly, Lx)) + <path>.json (step, dtau, seed, z0)."""

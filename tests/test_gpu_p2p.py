@@ -148,7 +148,7 @@ def test_p2p_ghost_trials_agree_across_ranks(gpu):
     the same schedule, and the trial steps are ordinary steps."""
     shape = (256, 16, 128)
     phi0 = _field0(shape)
-    script = [("upload", phi0), ("step", 340), ("ghost", None), ("field", None)]
+    script = [("upload", phi0), ("step", 390), ("ghost", None), ("field", None)]
     mono = _mono(shape, KW, script)
     outs = run_ranks(2, shape, KW, script)
     assert outs[0]["ghost"] == outs[1]["ghost"] and outs[0]["ghost"][0] in (4, 8, 16)
