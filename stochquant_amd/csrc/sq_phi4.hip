@@ -813,7 +813,11 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         float mp1;
         T2 = site_update4<NZ>(I1.row, lft, rgt, I1.hm, I1.hp, I0.row, I2.row, xa, A, A.fin != 0, K.m2v, &mp1);
         if constexpr (FR) {
-            frame_sites<NZ, true>(A, f1, T2, I1.row, xa, bmx, true, mp1);
+            // step s's records over the block's own rows and planes only: the
+            // halo rows and chunk-edge planes are recomputed copies of sites
+            // another block owns and records (the records are maxima, so the
+            // copies never changed them)
+            if (K.outw && p >= K.z0 && p < K.z1) frame_sites<NZ, true>(A, f1, T2, I1.row, xa, bmx, true, mp1);
             // the frame's snapshot: each output row's input at its owned planes, once
             if (A.snap != nullptr && K.outw && p + 1 >= K.z0 && p + 1 < K.z1)
                 __builtin_nontemporal_store(
@@ -1077,7 +1081,9 @@ __device__ __forceinline__ void tp_row(const Phi4StepArgs &A, const TbCtx &K, Tp
     }
     float mp1;
     T[tc] = site_update4<NZ>(I[ic], lft, rgt, up, dn, I[im], I[ip], xa, A, A.fin != 0, K.m2v, &mp1);
-    if constexpr (FR) frame_sites<NZ, true>(A, f1, T[tc], I[ic], xa, bmx, true, mp1);
+    if constexpr (FR) {  // own rows and planes only, as phi4_tb2_kernel
+        if (K.outw && k >= K.z0 && k < K.z1) frame_sites<NZ, true>(A, f1, T[tc], I[ic], xa, bmx, true, mp1);
+    }
     t_lds[sc][K.w][K.lane] = T[tc];
     // 4. B: step s+1 at plane k-1 from T(k-2), T(k-1), T(k) and T(k-1)'s
     //    y-neighbours, published in iteration k-1
