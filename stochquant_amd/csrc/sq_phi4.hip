@@ -300,6 +300,35 @@ __device__ __forceinline__ void frame_flush(const Phi4StepArgs &A, const FrameAc
     }
 }
 
+// Both step records of a fused launch in one pass (the two-step kernels):
+// wave maxima by DPP, combined across the block by LDS atomic maxima (fk / fa,
+// cleared at the kernel's start) behind ONE barrier, then one global atomic
+// per record.  Two frame_flush calls took four barriers and two serial folds
+// at every block's end: 10-20 us of a 20-step 256^3 frame
+// (profiles/r03/s2/fdiag/).  Maxima in any order: the same records.
+__device__ __forceinline__ void frame_flush2(const Phi4StepArgs &A, const FrameAcc &f1, const FrameAcc &f2,
+                                             unsigned long long *fk, uint32_t *fa) {
+    const bool bad = f1.am >= A.clampv || f2.am >= A.clampv;
+    if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
+    if (A.st_md == nullptr) return;  // a kernel argument: every thread returns here or none
+    const unsigned long long k1 = dpp_all_max_u64(((uint64_t)ord_f32(f1.m) << 32) | __float_as_uint(f1.d));
+    const unsigned long long k2 = dpp_all_max_u64(((uint64_t)ord_f32(f2.m) << 32) | __float_as_uint(f2.d));
+    const uint32_t a1 = (uint32_t)dpp_all_max_i((int)__float_as_uint(fminf(f1.am, A.clampv)));
+    const uint32_t a2 = (uint32_t)dpp_all_max_i((int)__float_as_uint(fminf(f2.am, A.clampv)));
+    if ((threadIdx.x & 63) == 0) {
+        atomicMax(&fk[0], k1);
+        atomicMax(&fk[1], k2);
+        atomicMax(&fa[0], a1);
+        atomicMax(&fa[1], a2);
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        const int slot = (int)threadIdx.x * kStabSlots + (int)(blockIdx.x % kStabSlots);
+        atomicMax(A.st_md + slot, fk[threadIdx.x]);
+        atomicMax(A.st_a + slot, fa[threadIdx.x]);
+    }
+}
+
 // Philox4x32-10 of the field-noise counters {q, cy, cz, cw} whose words 1..3
 // (stream, step lo, step hi) and key are wave-uniform, R independent q per
 // lane, round-major so the chains interleave.  The same function as
@@ -961,8 +990,14 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
     FrameAcc f1 = frame_acc(), f2 = frame_acc();  // steps s and s+1
     __shared__ float bmx[2];                        // the block's running maxima of both records (frame_sites)
+    __shared__ unsigned long long fk[2];            // frame_flush2's block maxima
+    __shared__ uint32_t fa[2];
     if constexpr (FR) {
-        if (threadIdx.x < 2) bmx[threadIdx.x] = -__builtin_inff();
+        if (threadIdx.x < 2) {
+            bmx[threadIdx.x] = -__builtin_inff();
+            fk[threadIdx.x] = 0ull;
+            fa[threadIdx.x] = 0u;
+        }
         __syncthreads();
     }
     TbRun R;
@@ -980,12 +1015,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
         if (p + 2 > z1) break;
         tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2, bmx);
     }
-    if constexpr (FR) {  // step s's records (the x-halo wave's sites are duplicates), then s+1's
-        __shared__ uint64_t sk[kTbWaves + 1];
-        __shared__ uint32_t sa[kTbWaves + 1];
-        frame_flush(A, f1, 0, sk, sa);
-        frame_flush(A, f2, 1, sk, sa);
-    }
+    if constexpr (FR) frame_flush2(A, f1, f2, fk, fa);  // step s's records, then s+1's
     block_end_stamp(A);
 }
 
@@ -1223,8 +1253,14 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
     const __amdgpu_buffer_rsrc_t p1 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 1), K.plane, K.pbytes);
     const __amdgpu_buffer_rsrc_t p2 = plane_rsrc(A.in, tb_pidx(A, K.z0), K.plane, K.pbytes);
     __shared__ float bmx[2];
-    if constexpr (FR) {
-        if (threadIdx.x < 2) bmx[threadIdx.x] = -__builtin_inff();
+    __shared__ unsigned long long fk[2];  // frame_flush2's block maxima
+    __shared__ uint32_t fa[2];
+    if constexpr (FR) {  // published by the prologue's barrier
+        if (threadIdx.x < 2) {
+            bmx[threadIdx.x] = -__builtin_inff();
+            fk[threadIdx.x] = 0ull;
+            fa[threadIdx.x] = 0u;
+        }
     }
     FrameAcc f1 = frame_acc(), f2 = frame_acc();
     TpRun R;
@@ -1279,12 +1315,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
             tp_xhalo<NZ, WH, 3>(A, K, R, k + 3, C, NB, tx);
         }
     }
-    if constexpr (FR) {
-        __shared__ uint64_t sk[kTbWaves + 1];
-        __shared__ uint32_t sa[kTbWaves + 1];
-        frame_flush(A, f1, 0, sk, sa);
-        frame_flush(A, f2, 1, sk, sa);
-    }
+    if constexpr (FR) frame_flush2(A, f1, f2, fk, fa);
     block_end_stamp(A);
 }
 
