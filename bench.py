@@ -18,14 +18,18 @@ Timing: first a clock-settle phase (--settle-ms of steps, untimed, reported as
 `settle_ms` / `settle_steps`: the short driver invocation --warmup 5 would
 otherwise time ramping clocks), then W warm-up steps, then EXACTLY K timed steps
 bracketed by barrier + device synchronisation; `value` = all site updates of
-all ranks / max over ranks of that wall time.  `roofline.achieved` = 8
-algorithmic bytes per site update x the updates of one launch
-/ the mean launch duration from one hipEvent pair on the kernel's own stream
-around the K timed steps (`frac_kernel`); `frac_wall` is the same bytes over
-the wall time behind `value`; `frac_real` is the real HBM bytes of a launch
-(the committed rocprofv3 PMC summary of this command) over the same launch time
--- the physical roofline, which the algorithmic figure (8 B per update, the
-fused kernel moving the field once per two updates) cannot show.
+all ranks / max over ranks of that wall time.
+
+Roofline: the dominant kernel is the two-step fused kernel,
+which moves the field once per two updates and is bound by VALU issue, not
+HBM.  `bound` "valu", `frac` = the launch's VALU-busy SIMD cycles (4 x
+SQ_ACTIVE_INST_VALU from the committed rocprofv3 PMC record of this same
+command, profiles/r04/driver_profile.json) / (1024 SIMDs x 2.4 GHz x the launch
+time measured here with dispatch events, as rocprofv3's kernel trace measures
+it).  Beside it: `frac_algorithmic` (8 B per site update, SURVEY.md §8d, over
+the same time -- saturates by construction under two-step temporal blocking),
+`frac_hbm_real` (the PMC bytes of a launch over that time) and
+`frac_algorithmic_wall` (8 B per update over the wall time behind `value`).
 
 Also in the line: `multi_rank_check` (stochquant_amd/verify.py: every rank's
 slab after a fixed check protocol against the golden digests of a single-GPU
@@ -79,6 +83,17 @@ def parse():
                     help="(tests) flip one value of this rank's slab before its check digest")
     ap.add_argument("--no-c3", action="store_true", help="skip the 512^3 (configs[2]) sub-record of the default run")
     ap.add_argument("--cpu-seconds-c3", type=float, default=8.0, help="target wall time of the 512^3 CPU sample")
+    ap.add_argument("--no-c1", action="store_true", help="skip the 32,768-site QM1D chain (configs[0]) sub-record")
+    ap.add_argument("--c1-frames", type=int, default=8, help="timed 1000-step frames of the C1 chain")
+    ap.add_argument("--cpu-loops-c1", type=int, default=200,
+                    help="steps of the C1 CPU sample (the reference's serial semantics on one core)")
+    ap.add_argument("--rank-timeout", type=float, default=None,
+                    help="deadline (s) for the whole run of every rank; on expiry rank 0 prints one JSON line with "
+                         "'error' and every rank's last phase and the ranks exit 3 (default: 300 s + 2 ms per "
+                         "step; 0 = none)")
+    ap.add_argument("--inject-stall", default=None,
+                    help="(tests) RANK:SECONDS -- this rank sleeps that long in its phase 'stall' after the "
+                         "rendezvous")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks and their process group, print each rank's slab and deep-halo "
                          "schedule, touch no GPU (tests the multi-rank launch path on a CPU host)")
@@ -112,33 +127,62 @@ def _free_port():
     return port
 
 
-def spawn_ranks(n):
+def rank_deadline(a):
+    """Seconds every rank of the run may take in all (--rank-timeout, 0 = none)."""
+    if a.rank_timeout is not None:
+        return a.rank_timeout
+    return 300.0 + 2e-3 * (a.steps + a.warmup)
+
+
+def spawn_ranks(n, deadline_s):
     """Start n rank processes of this script (no GPU call has been made here),
     relay rank 0's stdout, return the worst exit code.  A rank that fails ends
-    the others (they would otherwise wait in the rendezvous or a collective)."""
+    the others (they would otherwise wait in the rendezvous or a collective).
+    The ranks run their own deadline (stochquant_amd.rankwatch); 30 s after it
+    this parent kills them and prints the error line itself with every rank's
+    last reported phase."""
     import threading
+    from stochquant_amd import rankwatch
     port = str(_free_port())
+    pdir = rankwatch.phase_dir(port)
+    os.makedirs(pdir, exist_ok=True)
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port, SQ_PHASE_DIR=pdir)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
     out = []
     reader = threading.Thread(target=lambda: out.append(procs[0].stdout.read().decode()), daemon=True)
     reader.start()
+    t_end = time.time() + deadline_s + 30.0 if deadline_s > 0 else None
+    expired = False
     while any(p.poll() is None for p in procs):
         if any(p.poll() not in (None, 0) for p in procs):
-            for p in procs:
-                if p.poll() is None:
-                    p.kill()
+            break
+        if t_end is not None and time.time() > t_end:
+            expired = True
             break
         time.sleep(0.2)
+    phases = rankwatch.read_phases(pdir, n)
+    for p in procs:
+        if p.poll() is None:
+            p.kill()
     rcs = [p.wait() for p in procs]
     reader.join(timeout=10)
-    sys.stdout.write("".join(out))
+    text = "".join(out)
+    if expired and not any(l.startswith("{") for l in text.splitlines()):
+        text += rankwatch.error_line(METRIC, n, deadline_s, phases,
+                                     f"ranks did not finish within the deadline of {deadline_s:.0f} s + 30 s; "
+                                     f"killed by the spawning process") + "\n"
+    sys.stdout.write(text)
     sys.stdout.flush()
-    return max(rcs, key=abs)
+    if expired:
+        return rankwatch.EXIT_DEADLINE
+    # rank 0's own status first (its deadline exit is 3); the others were
+    # killed after it ended; a signal becomes 128 + signo
+    worst = rcs[0] if rcs[0] != 0 else max(rcs, key=abs)
+    return worst if worst >= 0 else 128 - worst
 
 
 def cpu_share():
@@ -188,24 +232,28 @@ def cpu_baseline(L, dtau, target_s):
                       f"{cores} threads = this job's CPU share of {os.cpu_count()} host CPUs), {dt:.2f} s"}
 
 
-def pmc_record(L, nranks, kernel):
-    """The committed rocprofv3 PMC summary for this workload and kernel, if any (it is
-    measured by scripts/pmc_r02.sh on this same command, not inside this run)."""
-    for name in (f"pmc_traffic_{L}.json", "pmc_traffic.json"):
-        path = os.path.join(ROOT, "profiles", name)
-        try:
-            with open(path) as fh:
-                d = json.load(fh)
-        except (OSError, ValueError):
-            continue
-        if d.get("size") == L:
-            break
-    else:
+PROFILE = os.path.join("profiles", "r04", "driver_profile.json")
+N_SIMD = 1024                   # 256 CUs x 4 SIMDs
+CLOCK_MHZ = 2400.0              # peak engine clock (MI355X_MICROARCH.md)
+VALU_PEAK = N_SIMD * CLOCK_MHZ / 1e3   # G SIMD-cycles/s: every SIMD issuing VALU every cycle
+
+
+def pmc_record(L, kernel):
+    """The committed rocprofv3 record of the driver's invocation for this lattice
+    (profiles/r04/driver_profile.json, made by scripts/r04_driver_prof.sh +
+    scripts/driver_profile.py from `python3 bench.py --steps 20 --warmup 5`,
+    not measured inside this run): PMC HBM bytes and VALU-busy cycles per launch
+    of the fused kernel, and its rocprof dispatch durations."""
+    path = os.path.join(ROOT, PROFILE)
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
         return None, None
-    k = kernel.split("<")[0]
-    if d.get("size") == L and d.get("nranks", 1) == nranks and k and k in d.get("kernel", ""):
-        return d, os.path.relpath(path, ROOT)
-    return None, None
+    rec = d.get("configs", {}).get(str(L))
+    if not rec or "tb2" not in kernel:
+        return None, None
+    return rec, PROFILE
 
 
 def make_lattice(a, shape, world, rank, local):
@@ -233,7 +281,7 @@ def make_lattice(a, shape, world, rank, local):
     return lat, (world > 1 or a.comm != "auto")
 
 
-def measure(a, lat, world, slab_path):
+def measure(a, lat, world, slab_path, watch=None):
     """Settle, warm-up, EXACTLY a.steps timed steps (barrier + device sync on both
     sides, max over ranks), then the roofline pass: the same steps again with one
     hipEvent pair on the step-kernel stream.  Returns (wall seconds, perf,
@@ -245,13 +293,19 @@ def measure(a, lat, world, slab_path):
         if world > 1:
             dist.barrier()
 
+    def phase(name):
+        if watch is not None:
+            watch.phase(name)
+
     if slab_path:
+        phase("trial_blocks")
         # setup: the timed trial blocks of the multi-rank slab path (one call long
         # enough for all of them), 3 x G steps per candidate (G, core pairs, rims)
         # in {(4,1,A), (8,1,A), (16,1,A), (16,0), (16,2|4,A|B), (16,1,A, other edge_first)}: 372 steps
         lat.step(400)
     # clock settle: untimed batches until settle_ms have passed on rank 0 (every
     # rank runs the same batches: the slab exchanges must pair up)
+    phase("settle")
     settle_steps = 0
     t_settle = time.perf_counter()
     while True:
@@ -264,6 +318,7 @@ def measure(a, lat, world, slab_path):
         if not int(go.item()):
             break
     settle_ms = (time.perf_counter() - t_settle) * 1e3
+    phase("warmup")
     lat.step(a.warmup)
     # host bookkeeping while the warm-up steps run, so the device idles only
     # for the one synchronisation before the timed region (an idle gap lets the
@@ -272,6 +327,7 @@ def measure(a, lat, world, slab_path):
     lat.set_profiling(0)
     torch.cuda.synchronize()
     barrier()
+    phase("timed")
     t0 = time.perf_counter()
     lat.step(a.steps)
     torch.cuda.synchronize()   # hipDeviceSynchronize: every stream of the library's slabs
@@ -280,12 +336,15 @@ def measure(a, lat, world, slab_path):
     lat.sync()                 # the library's own join + error check, outside the timed region
     perf = lat.perf()
     if not a.no_profile_events:
-        # roofline pass: the same K steps again, right behind, with ONE hipEvent
-        # pair on the step-kernel stream around their launches (mode 2; avg step
-        # = region / K, inter-kernel gaps included).  The pair's two marker
-        # packets cost ~12 us of wall per region (0.6 us per step at K = 20,
-        # profiles/r02/ab_events.log), so they stay out of the region `value`
-        # is timed on; per-launch dispatch events cost ~4 us per step.
+        phase("roofline_pass")
+        # roofline pass: the same K steps again, right behind the wall-timed
+        # region (whose launches carry no instrumentation), with ONE hipEvent
+        # pair on the step-kernel stream around their launches (mode 2; avg
+        # launch = region / launches, inter-kernel gaps included).  In one
+        # profiled run this mean agreed with rocprofv3's average dispatch
+        # duration of the same kernel within 0.6 % (32.16 vs 32.35 us), while
+        # per-launch dispatch events (mode 1) read 35.3 us: they perturb the
+        # launches they time (profiles/r04/README.md).
         lat.perf_reset()
         lat.set_profiling(2)
         torch.cuda.synchronize()
@@ -304,60 +363,78 @@ def measure(a, lat, world, slab_path):
 
 
 def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
-    """The bench line's roofline object for the dominant (step) kernel."""
+    """The bench line's roofline object for the dominant (step) kernel.
+
+    The fused two-step kernel is bound by VALU issue, not HBM:
+    it moves the field once per two updates, so 8 algorithmic bytes per update
+    over its time can exceed the HBM peak by construction.  For it `bound` is
+    "valu" and `frac` the physical fraction: the launch's VALU-busy SIMD cycles
+    (4 x SQ_ACTIVE_INST_VALU from the committed PMC record of this very
+    command) over 1024 SIMDs x 2.4 GHz x the launch time measured here.
+    `frac_algorithmic` keeps the contract's 8 B/update figure, `frac_hbm_real`
+    the PMC bytes of a launch over the same time."""
     value = float(sites_local * world) * a.steps / t if not a.strong else None
     launches = max(1, perf["kernel_launches"])
     spl = perf["steps"] * nslabs / launches          # steps per launch, measured (2 = two-step fused)
+    kname = lat.kernel_name
+    fused = "tb2" in kname and perf.get("fused_steps", 0) >= 0.5 * perf["steps"]
     if perf["step_kernel_launches"] > 0:
-        # event region on the (interior) step-kernel stream: it spans every
-        # launch of the timed steps, so charge all local sites to it
+        # one event pair on the (interior) step-kernel stream around the K steps:
+        # it spans every launch of them, so charge all local sites to it
         step_ms = perf["step_kernel_ms"] / perf["step_kernel_launches"]
+        timing = ("hipEvent pair on the kernel stream around a second pass of the same K steps right after the "
+                  "wall-timed region (region mean, inter-kernel gaps included)")
     else:
         step_ms = t * 1e3 / a.steps
+        timing = "wall clock"
     launch_ms = step_ms * spl
-    achieved = BYTES_PER_SITE * sites_local / (step_ms * 1e-3) / 1e9
-    kname = lat.kernel_name
-    rec, rec_path = pmc_record(L, world, kname) if not slab_path else (None, None)
-    fused = "tb2" in kname and perf.get("fused_steps", 0) >= 0.5 * perf["steps"]
-    r = {
-        # the fused kernel moves the field once per two updates (DESIGN.md §5)
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBPS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBPS, 4),
-        "frac_kernel": round(achieved / HBM_PEAK_GBPS, 4),
-        "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time",
-        "traffic": rec.get("hbm_bytes_per_launch") if rec else None,
-        "traffic_source": (f"cached: {rec_path}, rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes of this "
-                           f"bench command (not measured inside this run)") if rec else None,
-        "kernel": kname,
-        "timing": "hipEvent pair on the kernel stream around a second pass of the same K steps right "
-                  "after the wall-timed region (region mean)"
-                  if perf["step_kernel_launches"] > 0 else "wall clock",
-        "steps_per_launch": round(spl, 3),
-        "kernel_launches_timed": perf["kernel_launches"],
-        "algorithmic_bytes_per_launch": round(BYTES_PER_SITE * sites_local * spl),
-        "avg_launch_us": round(launch_ms * 1e3, 3),
-        "avg_step_us": round(step_ms * 1e3, 3),
-        # the least HBM traffic a launch can have (one read + one write
-        # of the field) and the rate it moved at
-        "hbm_min_bytes_per_launch": BYTES_PER_SITE * sites_local,
-        "hbm_min_GBps": round(BYTES_PER_SITE * sites_local / (launch_ms * 1e-3) / 1e9, 1),
-    }
+    alg = BYTES_PER_SITE * sites_local / (step_ms * 1e-3) / 1e9      # GB/s, 8 B per site update
+    rec, rec_path = pmc_record(L, kname) if (not slab_path and world == 1) else (None, None)
+    r = {"kernel": kname, "timing": timing, "steps_per_launch": round(spl, 3),
+         "kernel_launches_timed": perf["kernel_launches"],
+         "avg_launch_us": round(launch_ms * 1e3, 3), "avg_step_us": round(step_ms * 1e3, 3)}
+    valu = None
+    if fused and rec and rec.get("valu_busy_cycles_per_launch"):
+        valu = rec["valu_busy_cycles_per_launch"] / (launch_ms * 1e-3) / 1e9    # G SIMD-cycles/s
+    if fused and valu is not None:
+        r.update({
+            "bound": "valu",
+            "achieved": round(valu, 1),
+            "peak": VALU_PEAK,
+            "unit": "G VALU-busy SIMD-cycles/s",
+            "frac": round(valu / VALU_PEAK, 4),
+            "achieved_is": ("VALU-issue cycles of one launch (4 x SQ_ACTIVE_INST_VALU, committed PMC record of "
+                            "this command) / the launch time measured here; peak = 1024 SIMDs x 2.4 GHz"),
+        })
+    else:
+        r.update({
+            "bound": "valu" if fused else "hbm",
+            "achieved": round(alg, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(alg / HBM_PEAK_GBPS, 4),
+            "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time"
+                           + ("; no PMC record for this lattice: frac is the algorithmic figure" if fused else ""),
+        })
+    r["frac_algorithmic"] = round(alg / HBM_PEAK_GBPS, 4)
+    r["achieved_algorithmic_GBps"] = round(alg, 1)
+    r["algorithmic_bytes_per_launch"] = round(BYTES_PER_SITE * sites_local * spl)
+    r["hbm_min_bytes_per_launch"] = BYTES_PER_SITE * sites_local
+    r["traffic"] = rec.get("hbm_bytes_per_launch") if rec else None
     if rec:
-        # headroom the algorithmic figure cannot show (it counts 8 B per update,
-        # the fused kernel moves the field once per two): the real HBM bytes of
-        # a launch (PMC) over this run's launch time, the per-SIMD VALU issue
-        # utilisation and the launch busy fraction of the committed counters
+        r["traffic_source"] = (f"{rec_path}: rocprofv3 --pmc FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes of "
+                               f"`{json.load(open(os.path.join(ROOT, rec_path)))['command']}`, median per launch")
         tb = rec.get("hbm_bytes_per_launch")
         if tb:
-            r["real_GBps"] = round(tb / (launch_ms * 1e-3) / 1e9, 1)
-            r["frac_real"] = round(tb / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-        for k in ("valu_util_simd", "valu_issue_util_simd", "avg_resident_waves_per_simd", "valu_util_method",
-                  "pmc_kernel_us"):
+            r["achieved_hbm_real_GBps"] = round(tb / (launch_ms * 1e-3) / 1e9, 1)
+            r["frac_hbm_real"] = round(tb / (launch_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            r["traffic_over_hbm_min"] = round(tb / (BYTES_PER_SITE * sites_local), 4)
+        for k in ("valu_busy_cycles_per_launch", "valu_insts_per_wave", "avg_resident_waves_per_simd",
+                  "rocprof_avg_us", "rocprof_median_us", "valu_util_simd_at_rocprof_avg"):
             if rec.get(k) is not None:
-                r[k] = rec[k]
+                r["profile_" + k] = rec[k]
+        if rec.get("rocprof_avg_us"):
+            r["launch_us_vs_rocprof_avg"] = round(launch_ms * 1e3 / rec["rocprof_avg_us"], 4)
     if fused and not slab_path and world == 1:
         r.update(busy_fraction(lat))
     return r, value, fused
@@ -391,34 +468,125 @@ def cpu_baseline_c3(L, dtau, target_s):
         return {"error": str(e)[:200]}
 
 
+C1 = dict(N=32768, deltat=1.0, dtau=0.01, pot=0, C=1.0, loops=1000, seed=1)
+
+
+def c1_cpu_baseline(loops):
+    """The reference's own semantics for config C1 on one host core: the serial
+    restatement of one clEnqueueNDRangeKernel of time_dev (tau_kernel.cl:25-175,
+    oracle/orc_qm1d.c orc_serial_launch, shared LCG, in-order items) driven as
+    tauhost.c:479-560 (oracle.SerialChain), one frame of `loops` steps."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test/baseline infrastructure only: timed as the CPU baseline, never as the product
+    oracle.build()
+    N = C1["N"]
+    f0 = (2 * C1["dtau"]) ** 0.5 * np.random.default_rng(C1["seed"]).standard_normal(N)
+    ch = oracle.SerialChain(N, C1["deltat"], C1["dtau"], C1["pot"], C1["C"], loops, 12345, f0,
+                            omega=C1["deltat"] * (N // 2))
+    t0 = time.perf_counter()
+    ch.frame()
+    dt = time.perf_counter() - t0
+    return {"value": N * loops / dt, "unit": "site-updates/s", "cores": 1, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"one {loops}-step frame of the {N}-site chain under the reference's serial semantics "
+                      f"(oracle/orc_qm1d.c orc_serial_launch + tauhost.c's frame loop, oracle.SerialChain; "
+                      f"single-threaded, as the reference's one work-group), {dt:.2f} s"}
+
+
+def c1_record(a, local):
+    """BASELINE configs[0] / SURVEY.md §8d C1: the 32,768-site QM1D chain, 1000-step
+    Jacobi frames through the library (qm1d_frame_grid: the whole chip, one grid
+    barrier per step), f0 ~ N(0, 2 dtau), potID 0, C = 1.  Site-updates/s over
+    --c1-frames back-to-back frames (wall, one sync), the kernel time per frame
+    from dispatch events, and the CPU baseline of the reference's semantics."""
+    import numpy as np
+    import torch
+    from stochquant_amd import Qm1dChain
+    N, loops = C1["N"], C1["loops"]
+    f0 = (2 * C1["dtau"]) ** 0.5 * np.random.default_rng(C1["seed"]).standard_normal(N)
+    with Qm1dChain(N, C1["deltat"], C1["dtau"], pot=C1["pot"], C=C1["C"], loops=loops, seed=C1["seed"],
+                   device=local) as q:
+        q.upload(f0, omega=C1["deltat"] * (N // 2))
+        for _ in range(2):                   # warm-up: allocations, code objects, clocks
+            q.run_frame()
+        q.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        stable = [q.run_frame() for _ in range(a.c1_frames)]
+        q.sync()
+        t = time.perf_counter() - t0
+        q.perf_reset()
+        q.set_profiling(1)
+        for _ in range(a.c1_frames):
+            q.run_frame()
+        q.sync()
+        perf = q.perf()
+        q.set_profiling(0)
+        d = q.download()
+    kern_ms = perf["step_kernel_ms"] / max(1, a.c1_frames)
+    value = N * loops * a.c1_frames / t
+    alg = 48.0 * N * loops / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else None
+    return {
+        "config": {"workload": "QM1D chain, N = 32,768 sites (BASELINE configs[0] as SURVEY.md §8d C1), fp64, "
+                               "Jacobi order + Philox noise, one frame = 1000 Langevin steps",
+                   "N": N, "deltat": C1["deltat"], "dtau": C1["dtau"], "potID": C1["pot"], "C": C1["C"],
+                   "loops": loops, "f0": "sqrt(2 dtau) * normal (seed 1)"},
+        "value": value, "unit": "site-updates/s", "frames": a.c1_frames, "stable_frames": int(sum(stable)),
+        "ms_per_frame": t * 1e3 / a.c1_frames,
+        "kernel_ms_per_frame": round(kern_ms, 4),
+        "roofline": {"bound": "latency", "achieved": round(alg, 1) if alg else None, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(alg / HBM_PEAK_GBPS, 5) if alg else None,
+                     "achieved_is": "48 algorithmic B per site-step (f, x, xx0 read + written, fp64; SURVEY.md "
+                                    "§8d C1) / the frame kernels' dispatch-event time; the chain is bound by one "
+                                    "grid barrier + the fp64 divisions per step, not by memory (DESIGN.md §4)"},
+        "field_check": {"rms": float(np.sqrt(np.mean(d["f"] ** 2)))},
+        "cpu_baseline": None if a.no_cpu_baseline else c1_cpu_baseline(a.cpu_loops_c1),
+    }
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus > 1 and "RANK" not in os.environ:
-        sys.exit(spawn_ranks(a.gpus))
+        sys.exit(spawn_ranks(a.gpus, rank_deadline(a)))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
     a.gpus = world
+    from stochquant_amd import rankwatch
+    # every rank reports its phase and ends itself at the deadline (rank 0 first
+    # printing the error line with all ranks' phases): a hang in the first
+    # cross-device comm set-up or exchange must not leave the driver without a line
+    watch = rankwatch.Watch(rank, world, rank_deadline(a), METRIC)
     import torch
     import torch.distributed as dist
     from stochquant_amd import _lib, verify
     _lib.load()  # fail loudly if the HIP library is missing
     if world > 1:
+        watch.phase("rendezvous")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.inject_stall:
+        r_s, sec = a.inject_stall.split(":")
+        if int(r_s) == rank:
+            watch.phase("stall")
+            time.sleep(float(sec))
     if a.dry_run:
+        watch.phase("dry_run")
         dry_run(a, world, rank, local, dist)
         if world > 1:
             dist.destroy_process_group()
+        watch.finish()
         return
     torch.cuda.set_device(local)
     L = a.size
     shape = (L, L, L) if a.strong else (L, L, L * world)
+    watch.phase("comm_init", comm=a.comm, shape=list(shape))
     lat, slab_path = make_lattice(a, shape, world, rank, local)
     lat.init_field(0.1)
-    t, perf, settle_ms, settle_steps = measure(a, lat, world, slab_path)
+    t, perf, settle_ms, settle_steps = measure(a, lat, world, slab_path, watch)
     # sanity: the field stayed finite and bounded (no guard hits)
     m = lat.moments()
     sites_local = lat.nz_local * L * L
@@ -427,11 +595,12 @@ def main():
     nslabs = a.slabs if (world == 1 and a.comm == "loopback") else 1
     rl, _, fused = roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local)
     achieved_wall = BYTES_PER_SITE * value / 1e9
-    rl["frac_wall"] = round(achieved_wall / HBM_PEAK_GBPS, 4)
-    rl["achieved_wall"] = round(achieved_wall, 1)
+    rl["frac_algorithmic_wall"] = round(achieved_wall / HBM_PEAK_GBPS, 4)
+    rl["achieved_algorithmic_wall_GBps"] = round(achieved_wall, 1)
     # self-check (verify.py): the check protocol's slab digests against the
     # golden ones of a single-GPU run of the same global lattice, every rank
     check = "skipped"
+    watch.phase("check")
     if not a.no_check and a.dtau == verify.CHECK_PARAMS["dtau"]:
         d = verify.run_protocol(lat, corrupt=(rank == a.corrupt_rank))
         digests = [None] * world
@@ -498,6 +667,7 @@ def main():
             "field_check": {"rms": (m["sum2"] / sites_local) ** 0.5, "maxabs": m["maxabs"]},
         }
         if world == 1 and not a.no_cpu_baseline:
+            watch.phase("cpu_baseline")
             out["cpu_baseline"] = cpu_baseline(L, a.dtau, a.cpu_seconds)
         else:
             out["cpu_baseline"] = None
@@ -505,12 +675,13 @@ def main():
     # the same settle, warm-up and --steps, its own roofline and CPU sample
     if world == 1 and not a.strong and a.comm == "auto" and L == 256 and not a.no_c3:
         L3 = 512
+        watch.phase("c3_512")
         lat3, _ = make_lattice(a, (L3, L3, L3), 1, 0, local)
         lat3.init_field(0.1)
         t3, perf3, settle3, ssteps3 = measure(a, lat3, 1, False)
         sites3 = L3 ** 3
         rl3, value3, _ = roofline(a, lat3, L3, 1, False, t3, perf3, 1, sites3)
-        rl3["frac_wall"] = round(BYTES_PER_SITE * value3 / 1e9 / HBM_PEAK_GBPS, 4)
+        rl3["frac_algorithmic_wall"] = round(BYTES_PER_SITE * value3 / 1e9 / HBM_PEAK_GBPS, 4)
         m3 = lat3.moments()
         lat3.close()
         out["c3_512"] = {
@@ -523,9 +694,18 @@ def main():
             "field_check": {"rms": (m3["sum2"] / sites3) ** 0.5, "maxabs": m3["maxabs"]},
             "cpu_baseline": None if a.no_cpu_baseline else cpu_baseline_c3(L3, a.dtau, a.cpu_seconds_c3),
         }
+    # config C1 (BASELINE configs[0], the reference's own 1-D chain at 32,768 sites)
+    if out is not None and world == 1 and not a.strong and a.comm == "auto" and L == 256 and not a.no_c1:
+        watch.phase("c1_qm1d")
+        try:
+            out["c1_qm1d"] = c1_record(a, local)
+        except Exception as e:  # the headline record stands without it
+            out["c1_qm1d"] = {"error": str(e)[:300]}
     if world > 1:
+        watch.phase("teardown")
         dist.barrier()
         dist.destroy_process_group()
+    watch.finish()
     if out is not None:
         print(json.dumps(out), flush=True)
 

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SQ_ABI_VERSION 3
+#define SQ_ABI_VERSION 4
 
 /* status codes */
 #define SQ_OK 0

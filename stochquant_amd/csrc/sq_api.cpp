@@ -88,6 +88,8 @@ constexpr int kMbColl = 16;         // + q: rank q's contribution to collective 
 constexpr int kMbWords = 1024;
 constexpr int kP2pMaxRanks = kMbWords - kMbColl;
 constexpr unsigned int kP2pMagic = 0x53513250u;  // "SQ2P"
+// RCCL halo communicator: blocks per send/recv kernel (ncclConfig_t.maxCTAs)
+constexpr int kRcclMaxCtas = 0;
 
 struct Peer {  // a rank's buffers as this process addresses them
     float *stage = nullptr;
@@ -99,6 +101,9 @@ struct Peer {  // a rank's buffers as this process addresses them
 struct P2pBlob {  // sq_p2p_handle's output
     unsigned int magic, version;
     int rank, nranks, Lx, Ly, gpad, loops, gz, gauto;  // gz / gauto: active ghost depth, timed pick
+    // the block schedule: pinned settings and which of them the timed pick may
+    // change (the pick's candidate list and every exchange depend on them)
+    int ef_auto, k_auto, edge_first, core_pairs, rims_b;
     long long Lz, coll_cap;
     unsigned long long seed;
     hipIpcMemHandle_t stage, mbox, coll;
@@ -246,6 +251,26 @@ bool is_phi4(const sq_ctx *c) { return c->p.model == SQ_MODEL_PHI4; }
 // one slab per process, ranks of a job (RCCL or peer pointers)
 bool per_rank(int comm) { return comm == SQ_COMM_RCCL || comm == SQ_COMM_P2P; }
 
+// RCCL communicators are created non-blocking (ncclConfig_t.blocking = 0) so
+// that no call can hang the host: a call that returns ncclInProgress (the
+// init, a group end launching in the background) is polled with
+// ncclCommGetAsyncError up to a deadline (SQ_COMM_TIMEOUT_S, default 300 s);
+// past it the communicator is aborted (ncclCommAbort) and the call fails
+// with SQ_E_COMM instead of waiting forever on a peer that never comes.
+double comm_timeout_s() {
+    const char *e = getenv("SQ_COMM_TIMEOUT_S");
+    const double v = e ? atof(e) : 300.0;
+    return v > 0 ? v : 300.0;
+}
+
+int nccl_settle(sq_ctx *c, ncclResult_t r, const char *what);
+
+#define SQ_NCCLW(c, expr)                                                                        \
+    do {                                                                                         \
+        int rc_ = nccl_settle((c), (expr), #expr);                                               \
+        if (rc_ != SQ_OK) return rc_;                                                            \
+    } while (0)
+
 hipError_t wait_seq(hipStream_t s, unsigned int *word, unsigned int seq) {
     return hipStreamWaitValue32(s, word, seq, hipStreamWaitValueGte, 0xFFFFFFFFu);
 }
@@ -285,7 +310,38 @@ int rank_allreduce(sq_ctx *c, void *d, size_t n, sq::P2pRed red, hipStream_t st)
     case sq::P2pRed::kMaxF64: t = ncclFloat64; break;
     case sq::P2pRed::kSumF64: t = ncclFloat64; op = ncclSum; break;
     }
-    SQ_NCCL(ncclAllReduce(d, d, n, t, op, c->comm, st));
+    SQ_NCCLW(c, ncclAllReduce(d, d, n, t, op, c->comm, st));
+    return SQ_OK;
+}
+
+int nccl_settle(sq_ctx *c, ncclResult_t r, const char *what) {
+    if (r == ncclInProgress && c->comm != nullptr) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const double lim = comm_timeout_s();
+        long spins = 0;
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(c->comm, &st);
+            if (q != ncclSuccess) {
+                r = q;
+                break;
+            }
+            if (st != ncclInProgress) {
+                r = st;
+                break;
+            }
+            const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (el > lim) {
+                (void)ncclCommAbort(c->comm);
+                c->comm = nullptr;
+                return fail(SQ_E_COMM, std::string(what) + ": no completion within " + std::to_string((int)lim) +
+                                           " s (SQ_COMM_TIMEOUT_S); communicator aborted");
+            }
+            if (++spins > 2000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+            else std::this_thread::yield();
+        }
+    }
+    if (r != ncclSuccess) return fail(SQ_E_COMM, std::string(what) + ": " + ncclGetErrorString(r));
     return SQ_OK;
 }
 
@@ -676,12 +732,12 @@ int phi4_block(sq_ctx *c, int g) {
         const int P = c->p.nranks, r = c->p.rank;
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
         const size_t n = (size_t)G * plane;
-        SQ_NCCL(ncclGroupStart());
-        SQ_NCCL(ncclSend(src_hi[0], n, ncclFloat32, up, c->comm, s.sB));
-        SQ_NCCL(ncclSend(src_lo[0], n, ncclFloat32, dn, c->comm, s.sB));
-        SQ_NCCL(ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, s.sB));
-        SQ_NCCL(ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
-        SQ_NCCL(ncclGroupEnd());
+        SQ_NCCLW(c, ncclGroupStart());
+        SQ_NCCLW(c, ncclSend(src_hi[0], n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCLW(c, ncclSend(src_lo[0], n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCLW(c, ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, s.sB));
+        SQ_NCCLW(c, ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCLW(c, ncclGroupEnd());
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     }
@@ -825,6 +881,24 @@ int phi4_autotune(sq_ctx *c, int &n) {
 
 int phi4_steps_impl(sq_ctx *c, int n);
 
+// Multi-rank: one rank's unguarded upload makes the others' ghost planes
+// unguarded too, so after a local change of field_finite the ranks agree on it
+// (max-reduce of "not finite") before the next step call or frame uses it.
+int fin_agree(sq_ctx *c) {
+    if (!c->fin_sync) return SQ_OK;
+    c->fin_sync = false;
+    if (!per_rank(c->p.comm) || c->p.nranks <= 1) return SQ_OK;
+    hipStream_t st = c->slabs[0].sA;
+    double v = c->field_finite ? 0.0 : 1.0;
+    SQ_HIP(hipMemcpyAsync(c->dtune, &v, sizeof v, hipMemcpyHostToDevice, st));
+    int rc = rank_allreduce(c, c->dtune, 1, sq::P2pRed::kMaxF64, st);
+    if (rc) return rc;
+    SQ_HIP(hipMemcpyAsync(&v, c->dtune, sizeof v, hipMemcpyDeviceToHost, st));
+    SQ_HIP(hipStreamSynchronize(st));
+    c->field_finite = v == 0.0;
+    return SQ_OK;
+}
+
 // Every launch of the call reads c->field_finite as its `fin`; once one step
 // has run, every plane (ghost zones included: they are exchanged copies) has
 // been through the guard.
@@ -848,18 +922,9 @@ int phi4_steps_impl(sq_ctx *c, int n) {
     }
     if (c->p.comm == SQ_COMM_P2P && !c->p2p_ready)
         return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
-    if (c->fin_sync) {  // one rank's unguarded upload makes the others' ghost planes unguarded too
-        c->fin_sync = false;
-        if (per_rank(c->p.comm) && c->p.nranks > 1) {
-            hipStream_t st = c->slabs[0].sA;
-            double v = c->field_finite ? 0.0 : 1.0;
-            SQ_HIP(hipMemcpyAsync(c->dtune, &v, sizeof v, hipMemcpyHostToDevice, st));
-            int rc = rank_allreduce(c, c->dtune, 1, sq::P2pRed::kMaxF64, st);
-            if (rc) return rc;
-            SQ_HIP(hipMemcpyAsync(&v, c->dtune, sizeof v, hipMemcpyDeviceToHost, st));
-            SQ_HIP(hipStreamSynchronize(st));
-            c->field_finite = v == 0.0;
-        }
+    {
+        int rc = fin_agree(c);
+        if (rc) return rc;
     }
     if (c->g_auto && !c->g_tuned) {
         int rc = phi4_autotune(c, n);
@@ -1042,15 +1107,41 @@ int create_phi4(sq_ctx *c) {
         ncclUniqueId id;
         static_assert(sizeof(id.internal) <= 128, "ncclUniqueId size");
         memcpy(id.internal, p.comm_id, sizeof(id.internal));
-        SQ_NCCL(ncclCommInitRank(&c->comm, p.nranks, id, p.rank));
+        // non-blocking (bounded bring-up, nccl_settle) with the halo kernels'
+        // CU footprint capped: the exchange's send/recv kernel shares the CUs
+        // with the core pair it overlaps, so it gets
+        // SQ_RCCL_MAX_CTAS blocks (default kRcclMaxCtas; 0 = RCCL's choice)
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        const char *nb = getenv("SQ_RCCL_BLOCKING");
+        cfg.blocking = (nb && atoi(nb) != 0) ? 1 : 0;
+        const char *mc = getenv("SQ_RCCL_MAX_CTAS");
+        const int max_ctas = mc ? atoi(mc) : kRcclMaxCtas;
+        if (max_ctas > 0) {
+            cfg.maxCTAs = max_ctas;
+            cfg.minCTAs = 1;
+        }
+        ncclResult_t r = ncclCommInitRankConfig(&c->comm, p.nranks, id, p.rank, &cfg);
+        if (r != ncclSuccess && r != ncclInProgress) {
+            c->comm = nullptr;
+            return fail(SQ_E_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+        }
+        int rc = nccl_settle(c, r, "ncclCommInitRankConfig");
+        if (rc) return rc;
     }
     if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
-        SQ_HIP(hipMalloc(&c->mbox, kMbWords * sizeof(unsigned int)));
+        // fine-grained device memory: the words are written by the peers'
+        // command processors (hipStreamWriteValue32) and copy engines from
+        // other devices over xGMI and polled here by hipStreamWaitValue32 /
+        // read by the fold kernel -- in coarse-grained memory a reader may keep
+        // serving a stale cached line (round 3 recorded such a hang on a flag)
+        SQ_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->mbox), kMbWords * sizeof(unsigned int),
+                                     hipDeviceMallocFinegrained));
         SQ_HIP(hipMemset(c->mbox, 0, kMbWords * sizeof(unsigned int)));
         const size_t need = std::max({(size_t)8 * (size_t)c->Lz, (size_t)8 * sq::kStabSlots * (size_t)std::max(1, p.loops),
                                       (size_t)256});
         c->coll_cap = (need + 255) / 256 * 256;
-        SQ_HIP(hipMalloc(&c->coll, 2 * (size_t)p.nranks * c->coll_cap));
+        SQ_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->coll), 2 * (size_t)p.nranks * c->coll_cap,
+                                     hipDeviceMallocFinegrained));
         c->peers.assign(p.nranks, Peer{});
         c->peers[p.rank] = Peer{c->slabs[0].stage, c->mbox, c->coll, false};
         c->p2p_ready = p.nranks == 1;  // one rank: its own buffers, nothing to map
@@ -1299,13 +1390,30 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     const bool tables = c->N <= sq::kQm1dRegMaxN;
     if (tables) {  // the field-independent work of the frame, grid-wide ahead of the chain (qm1d_prep_launch)
         const size_t L = (size_t)c->p.loops, nq4 = (size_t)((c->N + 3) & ~3);
-        if (!c->qom) {
-            SQ_HIP(hipMalloc(&c->qom, sizeof(double) * (L + 1)));
-            SQ_HIP(hipMalloc(&c->qxi, sizeof(float) * L * nq4));
-            if (c->p.pot == 3) {
-                SQ_HIP(hipMalloc(&c->qtcl, sizeof(float) * L * (size_t)(c->N + 2)));
-                SQ_HIP(hipMalloc(&c->qdd, sizeof(double) * L * (size_t)c->N));
+        if (!c->qom) {  // all tables as one unit: a failed allocation leaves none behind
+            const size_t bxi = sizeof(float) * L * nq4;
+            const size_t btcl = c->p.pot == 3 ? sizeof(float) * L * (size_t)(c->N + 2) : 0;
+            const size_t bdd = c->p.pot == 3 ? sizeof(double) * L * (size_t)c->N : 0;
+            if (bxi + btcl + bdd > sq::kQm1dTableCap)
+                return fail(SQ_E_ARG, "QM1D frame tables (loops x N) exceed the device-memory cap "
+                                      "(sq::kQm1dTableCap); use fewer loops per frame");
+            double *om = nullptr, *dd = nullptr;
+            float *xi = nullptr, *tcl = nullptr;
+            hipError_t e = hipMalloc(&om, sizeof(double) * (L + 1));
+            if (e == hipSuccess) e = hipMalloc(&xi, bxi);
+            if (e == hipSuccess && btcl) e = hipMalloc(&tcl, btcl);
+            if (e == hipSuccess && bdd) e = hipMalloc(&dd, bdd);
+            if (e != hipSuccess) {
+                (void)hipFree(om);
+                (void)hipFree(xi);
+                (void)hipFree(tcl);
+                (void)hipFree(dd);
+                return fail(SQ_E_HIP, std::string("QM1D frame tables: hipMalloc: ") + hipGetErrorString(e));
             }
+            c->qom = om;
+            c->qxi = xi;
+            c->qtcl = tcl;
+            c->qdd = dd;
         }
         a.om = c->qom;
         a.xi = c->qxi;
@@ -1421,6 +1529,11 @@ int phi4_frame(sq_ctx *c, int *stable) {
     if (rc) return rc;
     c->in_frame = true;
     c->frame_step0 = c->step;
+    // the agreed value: a rollback restores it on every rank alike (an
+    // unagreed local value would let a rank with fin = 1 take the guard's fast
+    // path on a neighbour's unguarded ghost planes after the rollback)
+    rc = fin_agree(c);
+    if (rc) return rc;
     const bool fin0 = c->field_finite;
     rc = phi4_steps(c, c->p.loops);
     c->in_frame = false;
@@ -1431,11 +1544,11 @@ int phi4_frame(sq_ctx *c, int *stable) {
     Slab &s0 = c->slabs[0];
     if (per_rank(c->p.comm) && c->p.nranks > 1) {
         const bool grp = c->p.comm == SQ_COMM_RCCL;
-        if (grp) SQ_NCCL(ncclGroupStart());
+        if (grp) SQ_NCCLW(c, ncclGroupStart());
         rc = rank_allreduce(c, c->flag, 1, sq::P2pRed::kMaxI32, s0.sA);
         if (!rc) rc = rank_allreduce(c, c->st_md, nrec, sq::P2pRed::kMaxU64, s0.sA);
         if (!rc) rc = rank_allreduce(c, c->st_a, nrec, sq::P2pRed::kMaxU32, s0.sA);
-        if (grp) SQ_NCCL(ncclGroupEnd());
+        if (grp) SQ_NCCLW(c, ncclGroupEnd());
         if (rc) return rc;
     }
     // one read-back of the records and the flag into pinned memory
@@ -1510,7 +1623,13 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         if (rc) return rc;
         c->stab_init = true;
     }
-    if (!c->ctl) {
+    if (!c->ctl || !c->ctl_host || !c->rec_dev) {  // all three, or none after a failure
+        (void)hipFree(c->ctl);
+        (void)hipFree(c->rec_dev);
+        if (c->ctl_host) (void)hipHostFree(c->ctl_host);
+        c->ctl = nullptr;
+        c->rec_dev = nullptr;
+        c->ctl_host = nullptr;
         SQ_HIP(hipMalloc(&c->ctl, 2 * sizeof(sq::FrameCtl)));
         SQ_HIP(hipHostMalloc(&c->ctl_host, sizeof(sq::FrameCtl), hipHostMallocDefault));
         SQ_HIP(hipMalloc(&c->rec_dev, 3 * sizeof(float) * (size_t)L));
@@ -1522,6 +1641,10 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         (void)hipFree(c->fr_dtau);
         if (c->fr_stable_h) (void)hipHostFree(c->fr_stable_h);
         if (c->fr_dtau_h) (void)hipHostFree(c->fr_dtau_h);
+        c->fr_stable = nullptr;  // a failed allocation below must not leave freed pointers for sq_destroy
+        c->fr_dtau = nullptr;
+        c->fr_stable_h = nullptr;
+        c->fr_dtau_h = nullptr;
         c->fr_cap = 0;
         SQ_HIP(hipMalloc(&c->fr_stable, sizeof(int) * (size_t)m));
         SQ_HIP(hipMalloc(&c->fr_dtau, sizeof(double) * (size_t)m));
@@ -2290,6 +2413,11 @@ int sq_p2p_handle(sq_ctx *c, unsigned char out[SQ_P2P_HANDLE_BYTES]) {
     b.loops = c->p.loops;
     b.gz = c->gz;
     b.gauto = c->g_auto ? 1 : 0;
+    b.ef_auto = c->ef_auto ? 1 : 0;
+    b.k_auto = c->k_auto ? 1 : 0;
+    b.edge_first = c->edge_first ? 1 : 0;
+    b.core_pairs = c->core_pairs;
+    b.rims_b = c->rims_b ? 1 : 0;
     b.Lz = c->Lz;
     b.coll_cap = (long long)c->coll_cap;
     b.seed = c->p.seed;
@@ -2323,6 +2451,10 @@ int sq_p2p_connect(sq_ctx *c, const unsigned char *handles, int nranks) {
         if (b.loops != c->p.loops || b.gz != c->gz || b.gauto != (c->g_auto ? 1 : 0))
             return fail(SQ_E_ARG, "rank " + std::to_string(q) + " has different loops (" + std::to_string(b.loops) +
                                       "), active ghost depth (" + std::to_string(b.gz) + ") or ghost tuning (SQ_GHOST)");
+        if (b.ef_auto != (c->ef_auto ? 1 : 0) || b.k_auto != (c->k_auto ? 1 : 0) ||
+            b.edge_first != (c->edge_first ? 1 : 0) || b.core_pairs != c->core_pairs || b.rims_b != (c->rims_b ? 1 : 0))
+            return fail(SQ_E_ARG, "rank " + std::to_string(q) + " has a different block schedule (SQ_EDGE_FIRST, "
+                                      "SQ_CORE_PAIRS, SQ_RIMS_B must be set alike on every rank)");
     }
     DeviceGuard g(c->dev);
     for (int q = 0; q < nranks; ++q) {

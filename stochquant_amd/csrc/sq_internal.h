@@ -198,7 +198,10 @@ struct Qm1dArgs {
 int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant: N > kQm1dRegMaxN)
 constexpr int kQm1dMaxN = 1024 * 64;
 constexpr int kQm1dRegMaxN = 4096;  // register-resident frame kernel up to here; beyond, f ping-pong + scan scratch
-constexpr int kQm1dGridAux = 2048;  // N > kQm1dRegMaxN: xs and ds hold N + this many doubles (qm1d_frame_grid)
+constexpr int kQm1dGridAux = 2048;
+// device bytes the precomputed frame tables may take (loops x N x 4-16 B); a
+// frame longer than this at its N is refused rather than allocated
+constexpr size_t kQm1dTableCap = size_t(16) << 30;  // N > kQm1dRegMaxN: xs and ds hold N + this many doubles (qm1d_frame_grid)
 hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s);
 // The precomputed tables of a register-kernel frame (N <= kQm1dRegMaxN), on the
 // same stream ahead of qm1d_frame_launch; a.om / a.xi (/ a.tcl, a.dd) sized as above.

@@ -8,6 +8,7 @@
 // The Philox step counter is saved so a resumed run continues the same noise
 // stream; Δτ is restored (the reference caps it at argv Δτ on resume, :131-136,
 // which callers may apply).
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <exception>
@@ -148,12 +149,27 @@ static int save_field(sq_ctx *ctx, const char *path) {
     const std::string jpath = std::string(path) + ".json";
     FILE *fp = fopen(jpath.c_str(), "w");
     if (!fp) return io_fail("cannot write " + jpath);
+    // T and V exactly, as their IEEE bit patterns (a frame on an uploaded
+    // field with inf seeds V = inf, which is not a JSON number); the decimal
+    // values beside them are informative, null when not finite
+    char tv[2][32];
+    const float tvv[2] = {fs.T, fs.V};
+    for (int i = 0; i < 2; ++i) {
+        if (std::isfinite(tvv[i]))
+            snprintf(tv[i], sizeof tv[i], "%.9g", (double)tvv[i]);
+        else
+            snprintf(tv[i], sizeof tv[i], "null");
+    }
+    uint32_t tb, vb;
+    memcpy(&tb, &fs.T, sizeof tb);
+    memcpy(&vb, &fs.V, sizeof vb);
     fprintf(fp,
             "{\"format\": \"stochquant-phi4-slab\", \"version\": 1, \"dims\": [%lld, %lld, %lld], "
             "\"z0\": %lld, \"nz\": %lld, \"step\": %llu, \"dtau\": %.17g, \"seed\": %llu, "
-            "\"stab_init\": %d, \"stab_T\": %.9g, \"stab_V\": %.9g, \"stab_cnt\": %d}\n",
-            P.dims[0], P.dims[1], P.dims[2], z0, nz, step, dtau, P.seed, fs.init, (double)fs.T, (double)fs.V,
-            fs.stab_cnt);
+            "\"stab_init\": %d, \"stab_T\": %s, \"stab_V\": %s, \"stab_T_bits\": %u, \"stab_V_bits\": %u, "
+            "\"stab_cnt\": %d}\n",
+            P.dims[0], P.dims[1], P.dims[2], z0, nz, step, dtau, P.seed, fs.init, tv[0], tv[1], (unsigned)tb,
+            (unsigned)vb, fs.stab_cnt);
     return fclose(fp) == 0 ? SQ_OK : io_fail("cannot write " + jpath);
 }
 
@@ -198,8 +214,18 @@ static int load_field(sq_ctx *ctx, const char *path, int restore_counters) {
         const unsigned long long seed = json_uint(j, "seed", &f5);
         bool g1, g2, g3, g4;
         fs.init = (int)json_int(j, "stab_init", &g1);
-        fs.T = (float)json_dbl(j, "stab_T", &g2);
-        fs.V = (float)json_dbl(j, "stab_V", &g3);
+        bool b2, b3;
+        const unsigned long long tb = json_uint(j, "stab_T_bits", &b2);
+        const unsigned long long vb = json_uint(j, "stab_V_bits", &b3);
+        if (b2 && b3) {  // exact (files from round 4 on)
+            const uint32_t t32 = (uint32_t)tb, v32 = (uint32_t)vb;
+            memcpy(&fs.T, &t32, sizeof t32);
+            memcpy(&fs.V, &v32, sizeof v32);
+            g2 = g3 = true;
+        } else {
+            fs.T = (float)json_dbl(j, "stab_T", &g2);
+            fs.V = (float)json_dbl(j, "stab_V", &g3);
+        }
         fs.stab_cnt = (int)json_int(j, "stab_cnt", &g4);
         have_fs = g1 && g2 && g3 && g4;
         if (have_fs && fs.stab_cnt < 0) return io_fail("checkpoint stab_cnt must be >= 0");

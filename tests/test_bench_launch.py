@@ -45,3 +45,47 @@ def test_bench_single_rank_under_a_launcher():
     """RANK / WORLD_SIZE present (torch.distributed.run): no spawning."""
     d = _run(["--dry-run"], env={"RANK": "0", "WORLD_SIZE": "1", "LOCAL_RANK": "0"})
     assert d["n_gpus"] == 1 and d["ranks"][0]["plan"] is None
+
+
+def _run_rc(args, env=None, timeout=120):
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "SQ_PHASE_DIR"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def test_stalled_rank_ends_the_run_with_an_error_line():
+    """One rank stalls after the rendezvous (VERDICT r3 next #2a): rank 0's
+    deadline fires while it waits in the collective, it prints ONE JSON line
+    with "error" and every rank's last phase, and the run exits 3 within the
+    deadline (not at the driver's time limit)."""
+    import time
+    t0 = time.time()
+    r = _run_rc(["--gpus", "2", "--dry-run", "--inject-stall", "1:90", "--rank-timeout", "6"])
+    dt = time.time() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["value"] is None and "deadline" in d["error"] and d["n_gpus"] == 2
+    assert d["rank_phases"]["1"]["phase"] == "stall" and d["rank_phases"]["0"]["phase"] == "dry_run"
+    assert dt < 60, dt
+
+
+def test_stalled_rank_under_a_launcher(tmp_path):
+    """Launched as one rank by torch.distributed.run (no spawning parent): the
+    rank's own watchdog still prints the line and exits 3; a rank that never
+    reported shows as "no report"."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = {"RANK": "0", "WORLD_SIZE": "2", "LOCAL_RANK": "0", "SQ_PHASE_DIR": str(tmp_path),
+           "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)}
+    # rank 1 never starts: rank 0 waits in the rendezvous until its deadline
+    r = _run_rc(["--dry-run", "--rank-timeout", "5"], env=env)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["rank_phases"]["0"]["phase"] == "rendezvous" and d["rank_phases"]["1"]["phase"] == "no report"
