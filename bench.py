@@ -85,7 +85,7 @@ def parse():
     ap.add_argument("--cpu-seconds-c3", type=float, default=8.0, help="target wall time of the 512^3 CPU sample")
     ap.add_argument("--no-c1", action="store_true", help="skip the 32,768-site QM1D chain (configs[0]) sub-record")
     ap.add_argument("--c1-frames", type=int, default=8, help="timed 1000-step frames of the C1 chain")
-    ap.add_argument("--cpu-loops-c1", type=int, default=200,
+    ap.add_argument("--cpu-loops-c1", type=int, default=1000,
                     help="steps of the C1 CPU sample (the reference's serial semantics on one core)")
     ap.add_argument("--rank-timeout", type=float, default=None,
                     help="deadline (s) for the whole run of every rank; on expiry rank 0 prints one JSON line with "

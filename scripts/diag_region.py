@@ -26,7 +26,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=40)
     ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--flags", default="none", choices=["none", "auto", "spin", "yield", "block"],
+                    help="hipSetDeviceFlags schedule before the device is first used")
     a = ap.parse_args()
+    if a.flags != "none":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        fl = {"auto": 0, "spin": 1, "yield": 2, "block": 4}[a.flags]
+        rc = hip.hipSetDeviceFlags(ctypes.c_uint(fl))
+        print(json.dumps({"hipSetDeviceFlags": a.flags, "rc": rc}), flush=True)
     import torch
     from stochquant_amd import Phi4Lattice
     torch.cuda.set_device(0)
@@ -72,7 +80,8 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         rec("empty", (t1 - t0) * 1e6)
-    out = {k: round(statistics.median(v), 2) for k, v in res.items()}
+    out = {"flags": a.flags}
+    out.update({k: round(statistics.median(v), 2) for k, v in res.items()})
     for K in (2, 20, 200):
         out[f"overhead_{K}_us"] = round(out[f"wall_{K}"] - out[f"ev_{K}"], 2)
         out[f"wall_per_step_{K}"] = round(out[f"wall_{K}"] / K, 3)

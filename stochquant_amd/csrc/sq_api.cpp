@@ -221,10 +221,20 @@ struct sq_ctx {
     double *fr_dtau = nullptr, *fr_dtau_h = nullptr;
     int fr_cap = 0;
     bool dev_frames = false;  // the current frame's launches read {h, sig, sigq} from ctl_cur->coef
+    sq::FrameFoldArgs fold_next{};  // the next fused launch takes the previous frame's end (phi4_frames_dev)
+    sq::RecClear clr_next{};        // ... and the launch after it clears that frame's record set
+    bool clr_armed = false;
+    bool clr_first = false;         // ... armed by the next launch even without a fold (a batch's frame 0)
     sq::FrameCtl *ctl_cur = nullptr;
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
+    // slab paths: the fused launches that run beside an exchange (the core
+    // pairs, the middle pair after EDGES_DONE) aim at fewer blocks: the
+    // exchange's kernels hold a few CUs, and a full one-round grid then leaves
+    // its last blocks for a second round (core pair 43-45 us vs 33)
+    int tb_blocks_xchg = 480;
+    bool beside_xchg = false;       // the launch being issued runs beside an exchange
     long long ev_extra_steps = 0;   // profiling mode 1: steps beyond the first in timed launches
     ncclComm_t comm = nullptr;
     // SQ_COMM_P2P: mailbox, collective slots (2 parities x nranks x coll_cap
@@ -476,12 +486,29 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     c->snap_next = nullptr;
     a.stamps = c->stamps_next;  // sq_phi4_block_stamps
     c->stamps_next = nullptr;
+    // device frames: a folding first launch (it computes its own coefficients,
+    // so it must not read the ones its block 0 writes) arms the clear of the
+    // folded record set for the launch after it
+    if (c->clr_armed) {
+        a.clr = c->clr_next;
+        c->clr_armed = false;
+    }
+    if (c->fold_next.cin != nullptr) {
+        a.fold = c->fold_next;
+        a.dcoef = nullptr;
+        c->fold_next = sq::FrameFoldArgs{};
+        c->clr_armed = true;
+    } else if (c->clr_first) {  // a batch's first frame clears the set its second frame uses
+        c->clr_armed = true;
+    }
+    c->clr_first = false;
     // planes per block: pinned, or as many as make one round of tb_blocks
     // blocks (a ragged second round costs more than the deeper chunks), but
     // not fewer than 4 (a chunk recomputes 2 planes of the first step)
     const int nyg = c->Ly / 8, nxseg = c->Lx / 256;
     // (the slabs of a loopback decomposition run concurrently on their own streams)
-    const int nzc_t = std::max(1, c->tb_blocks / (nyg * nxseg * (int)c->slabs.size() * nr));
+    const int target = c->beside_xchg ? c->tb_blocks_xchg : c->tb_blocks;
+    const int nzc_t = std::max(1, target / (nyg * nxseg * (int)c->slabs.size() * nr));
     const int zb = c->tbz_pin ? c->tbz : std::min(len, std::max(4, (len + nzc_t - 1) / nzc_t));
     a.zlo = lo;
     a.zhi = nr == 2 ? hi2 : hi;
@@ -755,9 +782,14 @@ int phi4_block(sq_ctx *c, int g) {
         std::sort(starts.begin(), starts.end());
         starts.erase(std::unique(starts.begin(), starts.end()), starts.end());
         std::vector<char> timed(starts.size(), 0);
+        // stream-A launches issued while an exchange may run: from the block's
+        // exchange to its WAIT_EXCHANGE (the core pairs), and after EDGES_DONE
+        // (the middle pair, beside the next block's exchange)
+        bool xchg_live = true;
         for (const sq_block_op &op : ops) {
             int rc = SQ_OK;
             hipStream_t st = op.stream == kB ? s.sB : s.sA;
+            c->beside_xchg = xchg_live && op.stream != kB && c->p.comm != SQ_COMM_NONE;
             if (op.kind == SQ_OP_STEP || op.kind == SQ_OP_PAIR) {
                 const size_t gi = (size_t)(std::lower_bound(starts.begin(), starts.end(), op.step) - starts.begin());
                 const int in = cur ^ (int)(gi & 1);
@@ -771,6 +803,7 @@ int phi4_block(sq_ctx *c, int g) {
                 else
                     rc = phi4_launch_span(c, s, in, st, op.lo, op.hi, first);
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
+                if (op.stream != kB) xchg_live = false;
                 if (op.stream != kB) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));  // B: ordered behind its exchange
                 if (c->p.comm == SQ_COMM_LOOPBACK) {
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + ns - 1) % ns].evC, 0));
@@ -779,6 +812,7 @@ int phi4_block(sq_ctx *c, int g) {
             } else if (op.kind == SQ_OP_WAIT_STAGED) {
                 SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));
             } else if (op.kind == SQ_OP_EDGES_DONE) {
+                xchg_live = true;
                 SQ_HIP(hipEventRecord(s.evE, st));
             } else if (op.kind == SQ_OP_SIGNAL || op.kind == SQ_OP_WAIT) {
                 if (op.lo < 0 || op.lo >= kPlanSlots) return fail(SQ_E_STATE, "block op event slot out of range");
@@ -792,6 +826,7 @@ int phi4_block(sq_ctx *c, int g) {
             if (rc) return rc;
         }
         out_buf = cur ^ (int)(starts.size() & 1);
+        c->beside_xchg = false;
     }
     c->step = step0;
     for (int k = 0; k < g; ++k) count_step(c);
@@ -1206,6 +1241,9 @@ int create_phi4(sq_ctx *c) {
         // two blocks per CU (256-wide rows: 65 VGPRs, 10 waves; wider rows: 11 waves at <= 80)
         c->tb_blocks = 2 * std::max(1, ncu);
         if (const char *e = getenv("SQ_TB2_BLOCKS_PER_CU")) c->tb_blocks = std::max(1, atoi(e)) * std::max(1, ncu);
+        // 32 slots (16 CUs) left to the exchange's kernels; SQ_XCHG_BLOCKS pins the target
+        c->tb_blocks_xchg = std::max(1, c->tb_blocks - 32);
+        if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
@@ -1672,6 +1710,11 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     // other one, which the next frame then uses
     if (!c->frame_rec_zero) SQ_HIP(hipMemsetAsync(c->frame_cur, 0, c->frame_bytes, st));
     const bool snap_in_kernel = c->tbz > 0 && L >= 2;
+    // frame i > 0's first fused launch takes frame i-1's end (FrameFoldArgs):
+    // frames of 4..kFoldMaxL steps (the launch after the first, a fused pair
+    // too, clears the folded set); SQ_FRAME_FOLD=0 keeps one end launch per frame
+    const char *ff = getenv("SQ_FRAME_FOLD");
+    const bool fold = snap_in_kernel && L >= 4 && L <= sq::kFoldMaxL && !(ff && atoi(ff) == 0);
     for (int i = 0; i < m; ++i) {
         if (snap_in_kernel)
             c->snap_next = s0.snap;
@@ -1681,11 +1724,49 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         c->dev_frames = true;
         c->ctl_cur = c->ctl + (i & 1);
         c->frame_step0 = c->step;
+        c->clr_armed = false;
+        if (fold && i == 0 && m > 1) {
+            // the other record set still holds the previous batch's last frame:
+            // frame 0's second launch clears it for frame 1
+            const int cur_set = c->rec_set;
+            use_rec_set(c, cur_set ^ 1);
+            c->clr_next = sq::RecClear{c->st_md, c->st_a, c->flag, L * sq::kStabSlots};
+            use_rec_set(c, cur_set);
+            c->clr_first = true;
+        }
         int rc = phi4_steps(c, L);
         c->in_frame = false;
         c->dev_frames = false;
         c->snap_next = nullptr;
+        c->fold_next = sq::FrameFoldArgs{};
+        c->clr_armed = false;
+        c->clr_first = false;
         if (rc) return rc;
+        if (fold && i + 1 < m) {
+            // frame i+1's first launch decides frame i: it folds this record
+            // set and writes ctl[(i+1)&1]; frame i+1 accumulates into the other
+            // set (cleared by frame i's second launch)
+            sq::FrameFoldArgs fa{};
+            fa.cin = c->ctl + (i & 1);
+            fa.cout = c->ctl + ((i + 1) & 1);
+            fa.md = c->st_md;
+            fa.am = c->st_a;
+            fa.flag = c->flag;
+            fa.rec = c->rec_dev;
+            fa.stable_out = c->fr_stable + i;
+            fa.dtau_out = c->fr_dtau + i;
+            fa.snap = s0.snap;
+            fa.L = L;
+            sq::RecClear cl{};
+            cl.md = c->st_md;
+            cl.am = c->st_a;
+            cl.flag = c->flag;
+            cl.n = L * sq::kStabSlots;
+            use_rec_set(c, c->rec_set ^ 1);
+            c->fold_next = fa;
+            c->clr_next = cl;
+            continue;
+        }
         sq::FrameEndArgs e{};
         e.cin = c->ctl + (i & 1);
         e.cout = c->ctl + ((i + 1) & 1);

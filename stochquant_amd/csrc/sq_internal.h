@@ -35,6 +35,34 @@ int frame_state_set(sq_ctx *c, const FrameState &fs);
 // The gz planes on each side are the ghost zone (deep halo) of the
 // neighbouring slabs.  With periodic != 0 the slab is the whole lattice in z
 // (gz = 1, ghosts unused) and the kernel wraps z itself.
+struct FrameCtl;
+// Device frames (sq_run_frames): the first fused launch of frame f+1 takes
+// frame f's end itself -- every block folds frame f's records, applies the
+// stability rule and the Δτ controller to *cin (block 0 writes *cout, the
+// folded records, the verdict and Δτ), runs with the new coefficients, and
+// reads frame f's start snapshot instead of the field when the verdict is
+// unstable (the rollback without a copy); cin == nullptr: none.  The launch
+// after it clears the consumed record set (RecClear).  DESIGN.md §7.
+struct FrameFoldArgs {
+    const FrameCtl *cin;
+    FrameCtl *cout;
+    const unsigned long long *md;
+    const unsigned int *am;
+    const int *flag;
+    float *rec;
+    int *stable_out;
+    double *dtau_out;
+    const float *snap;  // frame f's start (interior planes, nz of them)
+    int L;
+};
+struct RecClear {  // zero n words of md and am and the flag (md == nullptr: none)
+    unsigned long long *md;
+    unsigned int *am;
+    int *flag;
+    int n;
+};
+constexpr int kFoldMaxL = 64;  // frames of at most this many steps fold (LDS: 12 B per step)
+
 struct Phi4StepArgs {
     const float *in;
     float *out;
@@ -69,6 +97,8 @@ struct Phi4StepArgs {
     // fused kernels (nullable): per block b, the constant 100 MHz clock
     // (s_memrealtime) at its start and end, stamps[2b], stamps[2b+1]
     unsigned long long *stamps;
+    FrameFoldArgs fold;  // frame instances of the fused kernels only
+    RecClear clr;
 };
 constexpr int kStabSlots = 32;
 

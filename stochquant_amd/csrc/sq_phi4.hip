@@ -628,6 +628,90 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, FrameA
 // come from the frame controller's state, which the previous frame's
 // controller kernel may have changed (the Δτ adapt of tauhost.c:523-541);
 // everything else from the launch.
+__device__ __forceinline__ float unord_f32_dev(uint32_t o);
+__device__ __forceinline__ void frame_decide(FrameCtl &c, float T, float V, int fired, int flag);
+
+// Device frames (FrameFoldArgs, sq_internal.h): the first fused launch of a
+// frame takes the previous frame's end -- the work of phi4_frame_end_kernel
+// without its launch.  Every block folds the kStabSlots-slot records into LDS
+// (u64 / u32 LDS atomic maxima: the same maxima as the end kernel's serial
+// fold), one thread applies the stability rule and frame_decide, and the block
+// runs with the coefficients and, when the verdict is unstable, the snapshot
+// as its input (the frame's rollback: the rejected field is never read
+// again, and the snapshot stays the start of the retried frame, so it is not
+// stored again).  Block 0 publishes the controller state, the folded records
+// and the verdict.  Any launch with clr.md set first zeroes that record set
+// (the one the previous launch folded; no block of this launch reads it).
+template <bool FR>
+__device__ __forceinline__ void frame_fold(Phi4StepArgs &A) {
+    if constexpr (FR) {
+        if (A.clr.md != nullptr) {
+            const int gt = (int)(blockIdx.x * blockDim.x + threadIdx.x), gs = (int)(gridDim.x * blockDim.x);
+            for (int q = gt; q < A.clr.n; q += gs) {
+                A.clr.md[q] = 0ull;
+                A.clr.am[q] = 0u;
+            }
+            if (gt == 0) *A.clr.flag = 0;
+        }
+        if (A.fold.cin == nullptr) return;
+        __shared__ unsigned long long sK[kFoldMaxL];
+        __shared__ unsigned int sAm[kFoldMaxL];
+        __shared__ float sCoef[3];
+        __shared__ int sSt;
+        const int L = A.fold.L;
+        for (int j = (int)threadIdx.x; j < L; j += (int)blockDim.x) {
+            sK[j] = 0ull;
+            sAm[j] = 0u;
+        }
+        __syncthreads();
+        for (int q = (int)threadIdx.x; q < L * kStabSlots; q += (int)blockDim.x) {
+            atomicMax(&sK[q / kStabSlots], A.fold.md[q]);
+            atomicMax(&sAm[q / kStabSlots], A.fold.am[q]);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            FrameCtl c = *A.fold.cin;
+            float T = c.T, V = c.V;
+            int fired = -1;
+            for (int j = 0; j < L; ++j) {  // stab_rule (sq_api.cpp)
+                const float M = unord_f32_dev((uint32_t)(sK[j] >> 32)), D = __uint_as_float((uint32_t)sK[j]);
+                const float Aj = __uint_as_float(sAm[j]);
+                const bool f = M > T && D > V;
+                T = M;
+                V = V < Aj ? Aj : V;
+                if (f) {
+                    fired = j;
+                    break;
+                }
+            }
+            frame_decide(c, T, V, fired, *A.fold.flag);
+            sCoef[0] = c.coef[0];
+            sCoef[1] = c.coef[1];
+            sCoef[2] = c.coef[2];
+            sSt = c.stable;
+            if (blockIdx.x == 0) {
+                *A.fold.cout = c;
+                if (A.fold.stable_out) *A.fold.stable_out = c.stable;
+                if (A.fold.dtau_out) *A.fold.dtau_out = c.dtau;
+            }
+        }
+        if (blockIdx.x == 0)
+            for (int j = (int)threadIdx.x; j < L; j += (int)blockDim.x) {
+                A.fold.rec[j] = unord_f32_dev((uint32_t)(sK[j] >> 32));
+                A.fold.rec[L + j] = __uint_as_float((uint32_t)sK[j]);
+                A.fold.rec[2 * L + j] = __uint_as_float(sAm[j]);
+            }
+        __syncthreads();
+        A.h = sCoef[0];
+        A.sig = sCoef[1];
+        A.sigq = sCoef[2];
+        if (!sSt) {
+            A.in = A.fold.snap - (size_t)A.gz * (size_t)A.Lx * (size_t)A.Ly;  // padded view of the snapshot
+            A.snap = nullptr;
+        }
+    }
+}
+
 template <bool FR>
 __device__ __forceinline__ Phi4StepArgs frame_args(const Phi4StepArgs &A0) {
     Phi4StepArgs A = A0;
@@ -908,7 +992,8 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
-    const Phi4StepArgs A = frame_args<FR>(A0);
+    Phi4StepArgs A = frame_args<FR>(A0);
+    frame_fold<FR>(A);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
@@ -1182,7 +1267,8 @@ __device__ __forceinline__ void tp_xhalo(const Phi4StepArgs &A, const TbCtx &K, 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A0) {
-    const Phi4StepArgs A = frame_args<FR>(A0);
+    Phi4StepArgs A = frame_args<FR>(A0);
+    frame_fold<FR>(A);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
@@ -1362,6 +1448,34 @@ __device__ __forceinline__ float unord_f32_dev(uint32_t o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7FFFFFFFu) : ~o);
 }
 
+// The host's frame verdict and Δτ controller (sq_api.cpp phi4_frame + adapt,
+// tauhost.c:523-529,537-541), operation for operation, on the controller state.
+__device__ __forceinline__ void frame_decide(FrameCtl &c, float T, float V, int fired, int flag) {
+    const int st = (flag == 0 && fired < 0) ? 1 : 0;
+    c.T = T;
+    c.V = V;
+    c.fired = fired;
+    c.flag = flag;
+    c.stable = st;
+    c.frames += 1;
+    if (c.adapt) {
+        if (st) {
+            if (c.stab_cnt > 10) {
+                c.stab_cnt = 0;
+                c.dtau /= 0.950;
+            }
+            c.stab_cnt += 1;
+        } else {
+            c.dtau *= 0.950;
+            c.stab_cnt = 0;
+        }
+    }
+    const float hf = (float)c.dtau;  // phi4_base_args
+    c.coef[0] = hf;
+    c.coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C);
+    c.coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C * kSqrt2Ln2);
+}
+
 __global__ __launch_bounds__(256) void phi4_frame_end_kernel(FrameEndArgs E) {
     __shared__ float sM[kEndChunk], sD[kEndChunk], sA[kEndChunk];
     __shared__ float sT, sV;
@@ -1415,28 +1529,7 @@ __global__ __launch_bounds__(256) void phi4_frame_end_kernel(FrameEndArgs E) {
     if (b0) {
         if (threadIdx.x == 0) {
             FrameCtl c = *E.cin;
-            c.T = sT;
-            c.V = sV;
-            c.fired = sFired;
-            c.flag = *E.flag;
-            c.stable = st;
-            c.frames += 1;
-            if (c.adapt) {  // adapt (sq_api.cpp), tauhost.c:523-529,537-541
-                if (st) {
-                    if (c.stab_cnt > 10) {
-                        c.stab_cnt = 0;
-                        c.dtau /= 0.950;
-                    }
-                    c.stab_cnt += 1;
-                } else {
-                    c.dtau *= 0.950;
-                    c.stab_cnt = 0;
-                }
-            }
-            const float hf = (float)c.dtau;  // phi4_base_args
-            c.coef[0] = hf;
-            c.coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C);
-            c.coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C * kSqrt2Ln2);
+            frame_decide(c, sT, sV, sFired, *E.flag);
             *E.cout = c;
             if (E.stable_out) *E.stable_out = st;
             if (E.dtau_out) *E.dtau_out = c.dtau;

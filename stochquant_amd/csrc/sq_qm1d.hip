@@ -599,7 +599,7 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
 // xs[N..] the block maxima, ds[N..] the two tagged words.
 constexpr int kGridT = 256;
 
-// Grid barrier of a cooperative launch (all blocks co-resident): thread 0 of
+// Grid barrier of a grid whose blocks are all co-resident: thread 0 of
 // each block releases its block's writes, counts the block in and spins until
 // every block of barrier `n` (1-based) has; the counter was zeroed ahead of the
 // launch.  A vector atomic and a relaxed load, no scalar-memory writes.
@@ -886,6 +886,20 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
                          : kk == 16 ? (const void *)qm1d_frame_grid<16>
                          : kk == 32 ? (const void *)qm1d_frame_grid<32>
                                     : (const void *)qm1d_frame_grid<4>;
+        if (q.gbar) {
+            // the counter barrier needs every block resident, not the
+            // cooperative-launch machinery (GWS, its own queue); a plain launch
+            // of G <= the chip's resident capacity (G = 16 at N = 32,768) keeps
+            // the frame on the context's stream like every other kernel, and
+            // profilers that mishandle cooperative dispatches at exit see none
+            int dev = 0, cus = 0, per_cu = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kGridT, 0);
+            if (e != hipSuccess) return e;
+            if (G > cus * per_cu) return hipErrorCooperativeLaunchTooLarge;
+            return hipLaunchKernel(fn, dim3(G), dim3(kGridT), args, 0, s);
+        }
         return hipLaunchCooperativeKernel(fn, dim3(G), dim3(kGridT), args, 0, s);
     }
     K = qm1d_sites_per_thread(a.N);

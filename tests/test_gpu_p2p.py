@@ -33,6 +33,12 @@ def _mono(shape, kw, script):
         for op, arg in script:
             if op == "upload":
                 L.upload(arg)
+            elif op == "upload_r0":   # arg = (field, nranks): rank 0's planes of field, the rest as they are
+                from stochquant_amd.decomp import slab_bounds
+                f = L.download()
+                z0, z1 = slab_bounds(shape[2], arg[1], 0)
+                f[z0:z1] = arg[0][z0:z1]
+                L.upload(f)
             elif op == "step":
                 L.step(arg)
             elif op == "frame":
@@ -174,6 +180,27 @@ def test_p2p_frames_rollback_and_correlator(gpu):
         assert o["TV"] == mono["TV"] and o["dtau"] == mono["dtau"]
         assert o["step_counter"] == mono["step_counter"]
         np.testing.assert_allclose(o["correlator"], mono["correlator"], rtol=1e-12, atol=1e-12)
+    assert np.array_equal(_assemble(outs), mono["field"][0])
+
+
+def test_p2p_rollback_after_one_rank_uploads_nan(gpu):
+    """only rank 0 uploads (a NaN on its top plane, next to rank 1's
+    ghost zone); the ranks agree that the field is unguarded before the frame,
+    so the rolled-back frame restores the agreed state on both and the next
+    frame's guard clamps the NaN on rank 1's ghost copies too: verdicts, dtau
+    and the field equal the single slab's."""
+    shape = (64, 16, 24)
+    kw = dict(KW, loops=4)
+    phi0 = _field0(shape)
+    bad = _field0(shape, seed=5)
+    bad[11, 3, 7] = np.nan
+    script = [("upload", phi0), ("step", 4), ("upload_r0", (bad, 2)), ("frame", None), ("frame", None),
+              ("field", None)]
+    mono = _mono(shape, kw, script)
+    assert mono["stable"] == [False, False]
+    outs = run_ranks(2, shape, kw, script, {"SQ_GHOST": "4"})
+    for o in outs:
+        assert o["stable"] == mono["stable"] and o["dtau"] == mono["dtau"] and o["TV"] == mono["TV"]
     assert np.array_equal(_assemble(outs), mono["field"][0])
 
 

@@ -575,6 +575,33 @@ def test_checkpoint_large_seed_and_frame_state(gpu, oracle_mod, tmp_path):
         assert np.array_equal(L.download(), full)
 
 
+def test_checkpoint_non_finite_frame_state_is_valid_json(gpu, oracle_mod, tmp_path):
+    """a frame on an uploaded field holding inf seeds V = inf (the
+    field's max |phi|); the checkpoint metadata must stay valid JSON (T / V as
+    null, their exact IEEE bits beside them) and a load must restore T and V
+    bit for bit."""
+    import json
+    shape = (256, 8, 12)
+    phi0 = _init(oracle_mod, shape, amp=0.3)
+    phi0[3, 2, 17] = np.inf
+    with _lat(shape, loops=4, dtau=0.01) as L:
+        L.upload(phi0)
+        L.run_frame()                     # the guard clamps the inf: rolled back, V seeded inf
+        st0 = L.stability(0)
+        assert not np.isfinite(st0["V"])
+        L.save(tmp_path / "ck.npy")
+    meta = json.loads((tmp_path / "ck.npy.json").read_text())   # strict JSON: no bare inf / nan
+    assert meta["stab_V"] is None
+    assert np.array([meta["stab_V_bits"]], np.uint32).view(np.float32)[0] == np.float32(st0["V"])
+    assert np.array([meta["stab_T_bits"]], np.uint32).view(np.float32)[0].tobytes() == \
+        np.float32(st0["T"]).tobytes()
+    with _lat(shape, loops=4, dtau=0.01) as L:
+        L.load(tmp_path / "ck.npy")
+        st = L.stability(0)
+        assert np.float32(st["V"]).tobytes() == np.float32(st0["V"]).tobytes()
+        assert np.float32(st["T"]).tobytes() == np.float32(st0["T"]).tobytes()
+
+
 def test_slice_correlator_across_slabs(gpu, oracle_mod):
     """The zero-momentum correlator of a decomposed lattice (loopback slabs;
     RCCL self-exchange = the all-reduce code path of the multi-rank case) equals
