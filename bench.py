@@ -94,6 +94,8 @@ def parse():
     ap.add_argument("--inject-stall", default=None,
                     help="(tests) RANK:SECONDS -- this rank sleeps that long in its phase 'stall' after the "
                          "rendezvous")
+    ap.add_argument("--inject-error", type=int, default=None,
+                    help="(tests) this rank raises after the rendezvous")
     ap.add_argument("--dry-run", action="store_true",
                     help="set up the ranks and their process group, print each rank's slab and deep-halo "
                          "schedule, touch no GPU (tests the multi-rank launch path on a CPU host)")
@@ -165,6 +167,14 @@ def spawn_ranks(n, deadline_s):
             break
         time.sleep(0.2)
     phases = rankwatch.read_phases(pdir, n)
+    # SIGTERM first: rank 0 then prints the line with every rank's phase
+    # (a failed rank's phase holds its error); SIGKILL what is left after 5 s
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    t_kill = time.time() + 5.0
+    while any(p.poll() is None for p in procs) and time.time() < t_kill:
+        time.sleep(0.1)
     for p in procs:
         if p.poll() is None:
             p.kill()
@@ -551,13 +561,22 @@ def main():
     if a.gpus > 1 and "RANK" not in os.environ:
         sys.exit(spawn_ranks(a.gpus, rank_deadline(a)))
     rank = int(os.environ.get("RANK", "0"))
-    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
-    a.gpus = world
     from stochquant_amd import rankwatch
     # every rank reports its phase and ends itself at the deadline (rank 0 first
     # printing the error line with all ranks' phases): a hang in the first
     # cross-device comm set-up or exchange must not leave the driver without a line
     watch = rankwatch.Watch(rank, world, rank_deadline(a), METRIC)
+    watch.on_sigterm()
+    try:
+        run(a, world, rank, watch)
+    except Exception as e:   # one line with the cause instead of a bare traceback
+        watch.fail(e)
+        raise
+
+
+def run(a, world, rank, watch):
+    local = 0 if a.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    a.gpus = world
     import torch
     import torch.distributed as dist
     from stochquant_amd import _lib, verify
@@ -568,6 +587,9 @@ def main():
         # one node by contract: RCCL's bootstrap over loopback (data moves over xGMI)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if a.inject_error is not None and a.inject_error == rank:
+        watch.phase("injected")
+        raise RuntimeError("injected failure (--inject-error)")
     if a.inject_stall:
         r_s, sec = a.inject_stall.split(":")
         if int(r_s) == rank:

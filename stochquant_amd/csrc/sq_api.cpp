@@ -62,7 +62,9 @@ struct DeviceGuard {
 
 struct Slab {
     float *buf[2] = {nullptr, nullptr};  // padded ping-pong
-    float *snap = nullptr;               // frame-start snapshot (interior planes)
+    float *snap = nullptr;               // frame-start snapshot (interior planes) = snap_pad + gpad planes
+    float *snap_pad = nullptr;           // its allocation, padded like buf[]: three-buffer device frames
+                                         // rotate the three (phi4_frames_dev)
     int nz = 0;
     long long z0 = 0;
     hipStream_t sA = nullptr, sB = nullptr;
@@ -224,6 +226,11 @@ struct sq_ctx {
     sq::FrameFoldArgs fold_next{};  // the next fused launch takes the previous frame's end (phi4_frames_dev)
     sq::RecClear clr_next{};        // ... and the launch after it clears that frame's record set
     bool clr_armed = false;
+    // three-buffer device frames (phi4_frames_dev): buffers of the batch, the
+    // frame's launch index, the controller state the launches read
+    bool tri = false;
+    float *tri_bufs[3] = {nullptr, nullptr, nullptr};
+    int frame_tk = 0;
     bool clr_first = false;         // ... armed by the next launch even without a fold (a batch's frame 0)
     sq::FrameCtl *ctl_cur = nullptr;
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
@@ -436,6 +443,13 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
         a.st_md = c->st_md + k;
         a.st_a = c->st_a + k;
     }
+    if (c->tri && c->in_frame) {  // the kernel picks in / out from the controller (FrameCtl::bs/bw0/bw1)
+        a.buf0 = c->tri_bufs[0];
+        a.buf1 = c->tri_bufs[1];
+        a.buf2 = c->tri_bufs[2];
+        a.tctl = c->ctl_cur;
+        a.tk = c->frame_tk++;
+    }
     return a;
 }
 
@@ -496,6 +510,7 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     if (c->fold_next.cin != nullptr) {
         a.fold = c->fold_next;
         a.dcoef = nullptr;
+        a.tctl = nullptr;  // it derives its buffers itself (frame_fold)
         c->fold_next = sq::FrameFoldArgs{};
         c->clr_armed = true;
     } else if (c->clr_first) {  // a batch's first frame clears the set its second frame uses
@@ -1535,6 +1550,16 @@ int stab_rule(float &T, float &V, const float *M, const float *D, const float *A
     return -1;
 }
 
+// The frame snapshot: allocated padded like the slab's buffers, so the three
+// can swap roles (three-buffer device frames); snap = its interior.
+int ensure_snap(sq_ctx *c, Slab &s) {
+    if (s.snap_pad) return SQ_OK;
+    const size_t bytes = (size_t)(s.nz + 2 * c->gpad) * plane_floats(c) * sizeof(float);
+    SQ_HIP(hipMalloc(&s.snap_pad, bytes));
+    s.snap = s.snap_pad + (size_t)c->gpad * plane_floats(c);
+    return SQ_OK;
+}
+
 int phi4_frame(sq_ctx *c, int *stable) {
     const size_t plane = plane_floats(c);
     // one slab without an exchange: every launch of the frame is on stream A,
@@ -1557,7 +1582,8 @@ int phi4_frame(sq_ctx *c, int *stable) {
     const bool snap_in_kernel = one_stream && c->tbz > 0 && c->p.loops >= 2;
     for (auto &s : c->slabs) {
         const size_t bytes = (size_t)s.nz * plane * sizeof(float);
-        if (!s.snap) SQ_HIP(hipMalloc(&s.snap, bytes));
+        rc = ensure_snap(c, s);
+        if (rc) return rc;
         if (snap_in_kernel)
             c->snap_next = s.snap;
         else
@@ -1672,7 +1698,10 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         SQ_HIP(hipHostMalloc(&c->ctl_host, sizeof(sq::FrameCtl), hipHostMallocDefault));
         SQ_HIP(hipMalloc(&c->rec_dev, 3 * sizeof(float) * (size_t)L));
     }
-    if (!s0.snap) SQ_HIP(hipMalloc(&s0.snap, nfl * sizeof(float)));
+    {
+        int rc = ensure_snap(c, s0);
+        if (rc) return rc;
+    }
     const int m = n - f;
     if (m > c->fr_cap) {
         (void)hipFree(c->fr_stable);
@@ -1705,6 +1734,21 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     h.adapt = c->p.adapt_dtau ? 1 : 0;
     h.stable = 1;
     h.fired = -1;
+    // three buffers (the slab's two and the padded snapshot allocation): a
+    // frame never writes the buffer it starts from, so that buffer is its
+    // rollback -- no snapshot store, no copy back (SQ_FRAME_TRI=0: off)
+    const char *ft = getenv("SQ_FRAME_TRI");
+    const bool tri = c->tbz > 0 && L >= 2 && !(ft && atoi(ft) == 0);
+    if (tri) {
+        c->tri_bufs[0] = s0.buf[c->cur];
+        c->tri_bufs[1] = s0.buf[c->cur ^ 1];
+        c->tri_bufs[2] = s0.snap_pad;
+        h.tri = 1;
+        h.bs = 0;
+        h.bw0 = 1;
+        h.bw1 = 2;
+        h.nl_odd = ((L / 2) + (L & 1)) & 1;  // launches per frame: the pairs and an odd last step
+    }
     SQ_HIP(hipMemcpyAsync(c->ctl, c->ctl_host, sizeof h, hipMemcpyHostToDevice, st));
     // the active record set must start zero; each frame-end launch clears the
     // other one, which the next frame then uses
@@ -1715,15 +1759,23 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     // too, clears the folded set); SQ_FRAME_FOLD=0 keeps one end launch per frame
     const char *ff = getenv("SQ_FRAME_FOLD");
     const bool fold = snap_in_kernel && L >= 4 && L <= sq::kFoldMaxL && !(ff && atoi(ff) == 0);
+    // diagnostic only (profiles/r04/frames/): no snapshot store, so a rolled-back
+    // frame restores garbage -- prices the store on stable frames
+    const char *dns = getenv("SQ_DIAG_NO_SNAP");
+    const bool diag_no_snap = dns && atoi(dns) != 0;
+    c->tri = tri;
     for (int i = 0; i < m; ++i) {
-        if (snap_in_kernel)
-            c->snap_next = s0.snap;
+        if (tri)
+            c->snap_next = nullptr;
+        else if (snap_in_kernel)
+            c->snap_next = diag_no_snap ? nullptr : s0.snap;
         else
             SQ_HIP(hipMemcpyAsync(s0.snap, plane0(c, s0, c->cur), nfl * sizeof(float), hipMemcpyDeviceToDevice, st));
         c->in_frame = true;
         c->dev_frames = true;
         c->ctl_cur = c->ctl + (i & 1);
         c->frame_step0 = c->step;
+        c->frame_tk = 0;
         c->clr_armed = false;
         if (fold && i == 0 && m > 1) {
             // the other record set still holds the previous batch's last frame:
@@ -1741,7 +1793,10 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         c->fold_next = sq::FrameFoldArgs{};
         c->clr_armed = false;
         c->clr_first = false;
-        if (rc) return rc;
+        if (rc) {
+            c->tri = false;
+            return rc;
+        }
         if (fold && i + 1 < m) {
             // frame i+1's first launch decides frame i: it folds this record
             // set and writes ctl[(i+1)&1]; frame i+1 accumulates into the other
@@ -1784,10 +1839,11 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         e.dtau_out = c->fr_dtau + i;
         e.dst = reinterpret_cast<float4 *>(plane0(c, s0, c->cur));
         e.snap = reinterpret_cast<const float4 *>(s0.snap);
-        e.n4 = (long long)(nfl / 4);
+        e.n4 = tri ? 0 : (long long)(nfl / 4);  // three buffers: the rollback is the next start buffer
         SQ_HIP(sq::phi4_frame_end_launch(e, st));
         c->perf.kernel_launches += 1;
     }
+    c->tri = false;
     c->frame_rec_zero = true;  // the active set is the one the last frame-end launch cleared
     SQ_HIP(hipMemcpyAsync(c->ctl_host, c->ctl + (m & 1), sizeof h, hipMemcpyDeviceToHost, st));
     SQ_HIP(hipMemcpyAsync(c->fr_stable_h, c->fr_stable, sizeof(int) * (size_t)m, hipMemcpyDeviceToHost, st));
@@ -1803,6 +1859,15 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
     c->stab_T = h.T;
     c->stab_V = h.V;
     c->stab_fired = h.fired;
+    if (tri) {  // the field is the start buffer of the frame after the batch: make it buf[0]
+        if (h.bs < 0 || h.bs > 2) return fail(SQ_E_STATE, "device frames: corrupt buffer rotation");
+        float *b[3] = {c->tri_bufs[h.bs], c->tri_bufs[(h.bs + 1) % 3], c->tri_bufs[(h.bs + 2) % 3]};
+        s0.buf[0] = b[0];
+        s0.buf[1] = b[1];
+        s0.snap_pad = b[2];
+        s0.snap = b[2] + (size_t)c->gpad * plane;
+        c->cur = 0;
+    }
     const float *r = static_cast<const float *>(c->frame_host);
     c->rec_M.assign(r, r + L);
     c->rec_D.assign(r + L, r + 2 * L);
@@ -1909,7 +1974,7 @@ int sq_destroy(sq_ctx *c) {
     for (auto &s : c->slabs) {
         (void)hipFree(s.buf[0]);
         (void)hipFree(s.buf[1]);
-        (void)hipFree(s.snap);
+        (void)hipFree(s.snap_pad);
         if (s.sA) (void)hipStreamDestroy(s.sA);
         if (s.sB) (void)hipStreamDestroy(s.sB);
         if (s.evC) (void)hipEventDestroy(s.evC);

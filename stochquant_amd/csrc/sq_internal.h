@@ -99,6 +99,12 @@ struct Phi4StepArgs {
     unsigned long long *stamps;
     FrameFoldArgs fold;  // frame instances of the fused kernels only
     RecClear clr;
+    // three-buffer device frames (frame instances): in / out are buf0..buf2 picked
+    // by the frame's launch index tk from *tctl (FrameCtl::bs / bw0 / bw1);
+    // tctl == nullptr: in / out as given
+    float *buf0, *buf1, *buf2;  // (named fields: a dynamic index would put the argument block in private memory)
+    const FrameCtl *tctl;
+    int tk;
 };
 constexpr int kStabSlots = 32;
 
@@ -117,6 +123,13 @@ struct FrameCtl {
     int fired;       // its firing step, -1 none
     int flag;        // its guard flag
     int frames;      // frames decided since the context's controller was (re)loaded
+    // three-buffer device frames (tri != 0; Phi4StepArgs::buf0..buf2): the frame
+    // starts from buffer bs, which no launch of the frame writes -- it IS the
+    // rollback snapshot -- and its launches alternate bs -> bw0 -> bw1 -> bw0
+    // ...; the frame's result is in bw0 when it has an odd number of launches
+    // (nl_odd), else bw1.  frame_decide rotates them: stable -> the next frame
+    // starts from the result, unstable -> from bs again.
+    int tri, bs, bw0, bw1, nl_odd;
 };
 // One launch after a frame (phi4_frame_end_kernel): folds the frame's
 // kStabSlots-slot records (md, am, flag), writes the per-step maxima to rec

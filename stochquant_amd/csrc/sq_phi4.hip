@@ -624,10 +624,15 @@ __device__ __forceinline__ void unit_run(const Phi4StepArgs &A, int unit, FrameA
     }
 }
 
-// Frames under device control (Phi4StepArgs::dcoef): the step coefficients
-// come from the frame controller's state, which the previous frame's
-// controller kernel may have changed (the Δτ adapt of tauhost.c:523-541);
-// everything else from the launch.
+// Buffer i of three-buffer frames by a select of scalars: the three are
+// separate kernel arguments (a select over an array's elements folds into a
+// dynamic index, and that puts the argument block in private memory).
+__device__ __forceinline__ uintptr_t pick_buf(const Phi4StepArgs &A, int i) {
+    const uintptr_t b0 = reinterpret_cast<uintptr_t>(A.buf0), b1 = reinterpret_cast<uintptr_t>(A.buf1),
+                    b2 = reinterpret_cast<uintptr_t>(A.buf2);
+    return i == 0 ? b0 : (i == 1 ? b1 : b2);
+}
+
 __device__ __forceinline__ float unord_f32_dev(uint32_t o);
 __device__ __forceinline__ void frame_decide(FrameCtl &c, float T, float V, int fired, int flag);
 
@@ -642,8 +647,18 @@ __device__ __forceinline__ void frame_decide(FrameCtl &c, float T, float V, int 
 // stored again).  Block 0 publishes the controller state, the folded records
 // and the verdict.  Any launch with clr.md set first zeroes that record set
 // (the one the previous launch folded; no block of this launch reads it).
+//
+// What a frame instance takes from the device instead of its launch
+// arguments: a few scalars, so the kernel's argument block is copied once at
+// the end (frame_args) -- a copy modified field by field across frame_fold's
+// barriers and loops stayed a 360-byte private-memory object (round 4).
+struct FrameOv {  // pointers as integers: the struct then stays in registers
+    uintptr_t in, out, snap;
+    float h, sig, sigq;
+};
+
 template <bool FR>
-__device__ __forceinline__ void frame_fold(Phi4StepArgs &A) {
+__device__ __forceinline__ void frame_fold(const Phi4StepArgs &A, FrameOv &ov) {
     if constexpr (FR) {
         if (A.clr.md != nullptr) {
             const int gt = (int)(blockIdx.x * blockDim.x + threadIdx.x), gs = (int)(gridDim.x * blockDim.x);
@@ -657,7 +672,7 @@ __device__ __forceinline__ void frame_fold(Phi4StepArgs &A) {
         __shared__ unsigned long long sK[kFoldMaxL];
         __shared__ unsigned int sAm[kFoldMaxL];
         __shared__ float sCoef[3];
-        __shared__ int sSt;
+        __shared__ int sSt, sBuf[2];
         const int L = A.fold.L;
         for (int j = (int)threadIdx.x; j < L; j += (int)blockDim.x) {
             sK[j] = 0ull;
@@ -689,6 +704,8 @@ __device__ __forceinline__ void frame_fold(Phi4StepArgs &A) {
             sCoef[1] = c.coef[1];
             sCoef[2] = c.coef[2];
             sSt = c.stable;
+            sBuf[0] = c.bs;
+            sBuf[1] = c.bw0;
             if (blockIdx.x == 0) {
                 *A.fold.cout = c;
                 if (A.fold.stable_out) *A.fold.stable_out = c.stable;
@@ -702,27 +719,59 @@ __device__ __forceinline__ void frame_fold(Phi4StepArgs &A) {
                 A.fold.rec[2 * L + j] = __uint_as_float(sAm[j]);
             }
         __syncthreads();
-        A.h = sCoef[0];
-        A.sig = sCoef[1];
-        A.sigq = sCoef[2];
-        if (!sSt) {
-            A.in = A.fold.snap - (size_t)A.gz * (size_t)A.Lx * (size_t)A.Ly;  // padded view of the snapshot
-            A.snap = nullptr;
-        }
+        // every field assigned unconditionally, by selects: stores to different
+        // fields on different paths get sunk into one store through a selected
+        // address, and the struct then lives in private memory
+        const bool tri = A.buf0 != nullptr, st = sSt != 0;
+        const uintptr_t snapv = reinterpret_cast<uintptr_t>(A.fold.snap) -
+                                sizeof(float) * (size_t)A.gz * (size_t)A.Lx * (size_t)A.Ly;  // padded view
+        const uintptr_t in = tri ? pick_buf(A, sBuf[0]) : (st ? ov.in : snapv);
+        const uintptr_t out = tri ? pick_buf(A, sBuf[1]) : ov.out;
+        const uintptr_t sn = (!tri && !st) ? uintptr_t(0) : ov.snap;
+        ov.in = in;
+        ov.out = out;
+        ov.snap = sn;
+        ov.h = sCoef[0];
+        ov.sig = sCoef[1];
+        ov.sigq = sCoef[2];
     }
 }
 
+// The arguments a launch runs with.  Frame instances under device control
+// (FR) take {h, sig, sigq} from the frame controller (dcoef: the Δτ adapt of
+// tauhost.c:523-541 the previous frame's end may have made), three-buffer
+// frames their in / out buffers (tctl), and a frame's first launch the
+// previous frame's end (frame_fold).
 template <bool FR>
 __device__ __forceinline__ Phi4StepArgs frame_args(const Phi4StepArgs &A0) {
-    Phi4StepArgs A = A0;
     if constexpr (FR) {
+        FrameOv ov{reinterpret_cast<uintptr_t>(A0.in), reinterpret_cast<uintptr_t>(A0.out),
+                   reinterpret_cast<uintptr_t>(A0.snap), A0.h, A0.sig, A0.sigq};
         if (A0.dcoef != nullptr) {
-            A.h = A0.dcoef[0];
-            A.sig = A0.dcoef[1];
-            A.sigq = A0.dcoef[2];
+            ov.h = A0.dcoef[0];
+            ov.sig = A0.dcoef[1];
+            ov.sigq = A0.dcoef[2];
         }
+        if (A0.tctl != nullptr) {  // three-buffer device frames: launch tk's buffers
+            const int bs = A0.tctl->bs, bw0 = A0.tctl->bw0, bw1 = A0.tctl->bw1;
+            const int bi = A0.tk == 0 ? bs : ((A0.tk & 1) ? bw0 : bw1);
+            const int bo = A0.tk == 0 ? bw0 : ((A0.tk & 1) ? bw1 : bw0);
+            const uintptr_t in = pick_buf(A0, bi), out = pick_buf(A0, bo);
+            ov.in = in;
+            ov.out = out;
+        }
+        frame_fold<FR>(A0, ov);
+        Phi4StepArgs A = A0;
+        A.in = reinterpret_cast<const float *>(ov.in);
+        A.out = reinterpret_cast<float *>(ov.out);
+        A.snap = reinterpret_cast<float *>(ov.snap);
+        A.h = ov.h;
+        A.sig = ov.sig;
+        A.sigq = ov.sigq;
+        return A;
+    } else {
+        return A0;
     }
-    return A;
 }
 
 // FR: a frame's launch (guard flag and stability records); the raw sq_step
@@ -992,8 +1041,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
-    Phi4StepArgs A = frame_args<FR>(A0);
-    frame_fold<FR>(A);
+    const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
@@ -1267,8 +1315,7 @@ __device__ __forceinline__ void tp_xhalo(const Phi4StepArgs &A, const TbCtx &K, 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A0) {
-    Phi4StepArgs A = frame_args<FR>(A0);
-    frame_fold<FR>(A);
+    const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
@@ -1474,6 +1521,14 @@ __device__ __forceinline__ void frame_decide(FrameCtl &c, float T, float V, int 
     c.coef[0] = hf;
     c.coef[1] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C);
     c.coef[2] = (float)(__builtin_sqrt(2.0 * (double)hf) * c.C * kSqrt2Ln2);
+    if (c.tri) {  // the next frame's buffers (FrameCtl): start, then the two others
+        const int fin = c.nl_odd ? c.bw0 : c.bw1;
+        const int third = 3 - c.bs - fin;
+        const int nbs = st ? fin : c.bs, nbw1 = st ? c.bs : fin;
+        c.bs = nbs;
+        c.bw0 = third;
+        c.bw1 = nbw1;
+    }
 }
 
 __global__ __launch_bounds__(256) void phi4_frame_end_kernel(FrameEndArgs E) {

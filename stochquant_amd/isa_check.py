@@ -76,3 +76,27 @@ def store_data_hazards(text, wait_states=2):
                     break
             ws += 1
     return found
+
+
+def kernel_metadata(lib):
+    """{kernel name: {"private": private_segment_fixed_size, "vgpr": vgpr_count,
+    "vgpr_spill": vgpr_spill_count}} from the code object's AMDGPU metadata."""
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "k.co")
+        subprocess.run([os.path.join(LLVM, "llvm-objcopy"), f"--dump-section=.hip_fatbin={fat}", lib,
+                        os.path.join(d, "x.o")], check=True, capture_output=True)
+        subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={fat}",
+                        f"--targets={TARGET}", f"--output={co}"], check=True, capture_output=True)
+        text = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", co], check=True, capture_output=True,
+                              text=True).stdout
+    out = {}
+    for block in text.split("    .name:")[1:]:
+        name = block.split()[0]
+        rec = {}
+        for key, field in (("private", ".private_segment_fixed_size"), ("vgpr", ".vgpr_count"),
+                           ("vgpr_spill", ".vgpr_spill_count")):
+            m = re.search(re.escape(field) + r":\s+(\d+)", block)
+            if m:
+                rec[key] = int(m.group(1))
+        out[name] = rec
+    return out

@@ -66,13 +66,38 @@ class Watch:
             threading.Thread(target=self._run, daemon=True, name="sq-rank-deadline").start()
 
     def phase(self, name, **info):
-        self.phase_name = name
+        if name != "error":
+            self.phase_name = name
         rec = {"rank": self.rank, "phase": name, "t": time.time(), "elapsed_s": round(time.time() - self.t0, 2)}
         rec.update(info)
         tmp = os.path.join(self.dir, f".rank{self.rank}.json.tmp")
         with open(tmp, "w") as fh:
             json.dump(rec, fh)
         os.replace(tmp, os.path.join(self.dir, f"rank{self.rank}.json"))
+
+    def fail(self, exc):
+        """This rank raised: record it for the others' reports; rank 0 prints the line."""
+        msg = f"{type(exc).__name__}: {exc}"[:400]
+        self.phase("error", error=msg, failed_in=self.phase_name)
+        if self.rank == 0:
+            print(error_line(self.metric, self.world, self.deadline_s, read_phases(self.dir, self.world),
+                             f"rank 0 failed: {msg}"), flush=True)
+        self.done.set()
+
+    def on_sigterm(self):
+        """Rank 0 killed by the launcher (torch.distributed.run ends every rank
+        once one has failed): print the line with every rank's phase first."""
+        import signal
+
+        def handler(signum, frame):
+            if not self.done.is_set():
+                self.done.set()
+                print(error_line(self.metric, self.world, self.deadline_s, read_phases(self.dir, self.world),
+                                 f"rank {self.rank} terminated (signal {signum}) in phase '{self.phase_name}'"),
+                      flush=True)
+            os._exit(128 + signum)
+        if self.rank == 0:
+            signal.signal(signal.SIGTERM, handler)
 
     def finish(self):
         self.phase("done")

@@ -23,9 +23,12 @@ def rank_main(conn, rank, nranks, shape, kw, env, script):
         for op, arg in script:
             if op == "upload":
                 lat.upload(arg[lat.z0:lat.z0 + lat.nz_local])
-            elif op == "upload_r0":   # only rank 0 uploads (its slab of arg = (field, nranks))
+            elif op == "upload_r0":   # rank 0 uploads its slab of arg = (field, nranks); the others
+                                      # re-upload their own slab (uploads are collective, stochquant.h)
                 if rank == 0:
                     lat.upload(arg[0][lat.z0:lat.z0 + lat.nz_local])
+                else:
+                    lat.upload(lat.download())
             elif op == "step":
                 lat.step(arg)
             elif op == "frame":

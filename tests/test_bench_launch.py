@@ -89,3 +89,16 @@ def test_stalled_rank_under_a_launcher(tmp_path):
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     assert d["rank_phases"]["0"]["phase"] == "rendezvous" and d["rank_phases"]["1"]["phase"] == "no report"
+
+
+def test_failing_rank_reports_its_error():
+    """A rank that raises (after the rendezvous) ends the spawned run at once:
+    the parent terminates the others, and rank 0's line carries the failed
+    rank's phase and message."""
+    r = _run_rc(["--gpus", "2", "--dry-run", "--inject-error", "1", "--rank-timeout", "60"])
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, (r.stdout, r.stderr[-2000:])
+    d = json.loads(lines[0])
+    assert d["value"] is None and "terminated" in d["error"]
+    assert d["rank_phases"]["1"]["phase"] == "error" and "injected" in d["rank_phases"]["1"]["error"]

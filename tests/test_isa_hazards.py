@@ -34,3 +34,20 @@ def test_checker_sees_the_round2_pattern():
 """
     bad = isa_check.store_data_hazards(text)
     assert len(bad) == 1 and bad[0][3] == 0 and "v[2:5]" in bad[0][1]
+
+
+def test_hot_kernels_use_no_private_memory(sqlib):
+    """The raw and frame instances of the 256-wide fused kernel and of the
+    per-step kernel keep their state in registers: round 4's frame fold first
+    put the 360-byte argument block (then a 24-byte override pair whose stores
+    the compiler had merged) in private memory, and the frame launches ran 4x
+    slower.  The wide-row instances with a 6-wave budget are allowed their
+    documented small spills."""
+    from stochquant_amd import isa_check
+    md = isa_check.kernel_metadata(os.path.join(ROOT, "stochquant_amd", "lib", "libstochquant.so"))
+    hot = {k: v for k, v in md.items()
+           if ("phi4_tb2_kernelILb1ELb0E" in k or "phi4_tb2p_kernelILb1ELb0E" in k
+               or "phi4_step_kernelILi64ELi1ELi1E" in k)}
+    assert len(hot) >= 8, sorted(md)[:20]
+    bad = {k: v for k, v in hot.items() if v.get("private", 0) != 0}
+    assert bad == {}, bad
