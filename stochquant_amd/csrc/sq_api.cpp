@@ -240,8 +240,19 @@ struct sq_ctx {
     // pairs, the middle pair after EDGES_DONE) aim at fewer blocks: the
     // exchange's kernels hold a few CUs, and a full one-round grid then leaves
     // its last blocks for a second round (core pair 43-45 us vs 33)
-    int tb_blocks_xchg = 480;
+    int tb_blocks_xchg = 416;
     bool beside_xchg = false;       // the launch being issued runs beside an exchange
+    // gated pair 0 (SQ_SLAB_GATE, default on): K = 1 blocks run the core pair and
+    // the rim pair as ONE launch whose thin rim chunks wait in-kernel for the
+    // exchange (Phi4StepArgs::gate), no WAIT_EXCHANGE hop and no small rim grid
+    bool slab_gate = false;
+    unsigned int *gate_word = nullptr;  // fine-grained: stream B writes ++gate_seq behind each exchange
+    unsigned int gate_seq = 0;
+    int *gate_err = nullptr;
+    struct {
+        bool on;
+        int tlo0, thi0, tlen;
+    } gate_next{false, 0, 0, 0};
     long long ev_extra_steps = 0;   // profiling mode 1: steps beyond the first in timed launches
     ncclComm_t comm = nullptr;
     // SQ_COMM_P2P: mailbox, collective slots (2 parities x nranks x coll_cap
@@ -536,6 +547,18 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     a.nxseg = nxseg;
     a.nyg = nyg;
     a.nunits = a.nxseg * a.nyg * a.nzc;
+    if (c->gate_next.on) {  // the rim ranges as thin gated chunks of this launch
+        a.gate = c->gate_word;
+        a.gate_seq = c->gate_seq;
+        a.gate_err = c->gate_err;
+        a.n_reg = a.nunits;
+        a.tzc = 4;
+        a.tlen = c->gate_next.tlen;
+        a.tlo0 = c->gate_next.tlo0;
+        a.thi0 = c->gate_next.thi0;
+        a.ntz = (a.tlen + a.tzc - 1) / a.tzc;
+        c->gate_next.on = false;
+    }
     EvPair *e = nullptr;
     if (timed && c->profiling == 1) {
         int rc = ev_take(c, &e);
@@ -688,6 +711,20 @@ std::vector<sq_block_op> block_plan(int nz, int G, int g, bool fuse2, bool edge_
     return ops;
 }
 
+// The index of a plan's [PAIR core (A), WAIT_EXCHANGE (A), PAIR rim (A, two
+// equal ranges)] of one step -- the K = 1, rims-on-A block start -- or -1.
+int gate_pattern(const std::vector<sq_block_op> &ops) {
+    for (size_t i = 0; i + 2 < ops.size(); ++i) {
+        const sq_block_op &a = ops[i], &w = ops[i + 1], &r = ops[i + 2];
+        if (a.kind == SQ_OP_PAIR && a.stream == kA && a.lo2 >= a.hi2 && w.kind == SQ_OP_WAIT_EXCHANGE &&
+            w.stream == kA && r.kind == SQ_OP_PAIR && r.stream == kA && r.step == a.step && r.lo2 < r.hi2 &&
+            r.hi - r.lo == r.hi2 - r.lo2)
+            return (int)i;
+        if (a.kind == SQ_OP_WAIT_EXCHANGE) return -1;  // the pattern is the block's start or absent
+    }
+    return -1;
+}
+
 // Deep-halo block of g <= gz steps on every slab: executes block_plan.
 int phi4_block(sq_ctx *c, int g) {
     const size_t plane = plane_floats(c);
@@ -783,6 +820,10 @@ int phi4_block(sq_ctx *c, int g) {
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     }
+    // gated pair 0: the exchange's completion as a device word the rim chunks poll
+    const bool gated = c->slab_gate && c->gate_word != nullptr && ns == 1 && per_rank(c->p.comm) &&
+                       gate_pattern(plans[0]) >= 0;
+    if (gated) SQ_HIP(hipStreamWriteValue32(c->slabs[0].sB, c->gate_word, ++c->gate_seq, 0));
     // 2. the rest of the schedule, slab by slab (each slab has its own streams;
     //    slabs of a loopback decomposition may differ in nz, hence in schedule)
     int out_buf = cur;
@@ -801,10 +842,28 @@ int phi4_block(sq_ctx *c, int g) {
         // exchange to its WAIT_EXCHANGE (the core pairs), and after EDGES_DONE
         // (the middle pair, beside the next block's exchange)
         bool xchg_live = true;
-        for (const sq_block_op &op : ops) {
+        for (size_t oi = 0; oi < ops.size(); ++oi) {
+            const sq_block_op &op = ops[oi];
             int rc = SQ_OK;
             hipStream_t st = op.stream == kB ? s.sB : s.sA;
             c->beside_xchg = xchg_live && op.stream != kB && c->p.comm != SQ_COMM_NONE;
+            // gated pair 0: [PAIR core (A), WAIT_EXCHANGE (A), PAIR rim (A, two ranges)] of the
+            // same step as one launch whose rim chunks wait in-kernel for the exchange
+            if (gated && (int)oi == gate_pattern(ops)) {
+                const sq_block_op &rim = ops[oi + 2];
+                const size_t gi = (size_t)(std::lower_bound(starts.begin(), starts.end(), op.step) - starts.begin());
+                const int in = cur ^ (int)(gi & 1);
+                const bool first = !timed[gi];
+                timed[gi] = 1;
+                c->step = step0 + (unsigned long long)op.step;
+                c->gate_next = {true, rim.lo, rim.lo2, rim.hi - rim.lo};
+                rc = phi4_tb2_range(c, s, in, st, op.lo, op.hi, 0, 0, 0, first);
+                c->gate_next.on = false;
+                if (rc) return rc;
+                xchg_live = false;
+                oi += 2;
+                continue;
+            }
             if (op.kind == SQ_OP_STEP || op.kind == SQ_OP_PAIR) {
                 const size_t gi = (size_t)(std::lower_bound(starts.begin(), starts.end(), op.step) - starts.begin());
                 const int in = cur ^ (int)(gi & 1);
@@ -1178,6 +1237,14 @@ int create_phi4(sq_ctx *c) {
         int rc = nccl_settle(c, r, "ncclCommInitRankConfig");
         if (rc) return rc;
     }
+    if (per_rank(p.comm)) {  // the gated pair 0's word (fine-grained: written by stream B, polled by kernels)
+        SQ_HIP(hipExtMallocWithFlags(reinterpret_cast<void **>(&c->gate_word), 64, hipDeviceMallocFinegrained));
+        SQ_HIP(hipMemset(c->gate_word, 0, 64));
+        SQ_HIP(hipMalloc(&c->gate_err, sizeof(int)));
+        SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
+        const char *e = getenv("SQ_SLAB_GATE");
+        c->slab_gate = e ? atoi(e) != 0 : true;
+    }
     if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
         // fine-grained device memory: the words are written by the peers'
         // command processors (hipStreamWriteValue32) and copy engines from
@@ -1256,8 +1323,10 @@ int create_phi4(sq_ctx *c) {
         // two blocks per CU (256-wide rows: 65 VGPRs, 10 waves; wider rows: 11 waves at <= 80)
         c->tb_blocks = 2 * std::max(1, ncu);
         if (const char *e = getenv("SQ_TB2_BLOCKS_PER_CU")) c->tb_blocks = std::max(1, atoi(e)) * std::max(1, ncu);
-        // 32 slots (16 CUs) left to the exchange's kernels; SQ_XCHG_BLOCKS pins the target
-        c->tb_blocks_xchg = std::max(1, c->tb_blocks - 32);
+        // 96 slots left to the exchange's kernels: RCCL self-exchange, 256^3, G = 16
+        // (profiles/r04/slab/): 512 blocks 19.36 / 19.54 us/step, 480 19.49 / 19.47,
+        // 448 19.02 / 19.32, 416 18.89 / 19.24; SQ_XCHG_BLOCKS pins the target
+        c->tb_blocks_xchg = std::max(1, c->tb_blocks - 96);
         if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
@@ -1970,6 +2039,8 @@ int sq_destroy(sq_ctx *c) {
         }
     (void)hipFree(c->mbox);
     (void)hipFree(c->coll);
+    (void)hipFree(c->gate_word);
+    (void)hipFree(c->gate_err);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &s : c->slabs) {
         (void)hipFree(s.buf[0]);
@@ -2215,7 +2286,14 @@ int sq_sync(sq_ctx *c) {
     if (!c) return fail(SQ_E_ARG, "null context");
     DeviceGuard g(c->dev);
     if (c->qstream) SQ_HIP(hipStreamSynchronize(c->qstream));
-    return phi4_join(c);
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    if (c->gate_err) {  // a gated rim chunk gave up waiting for its exchange (tb_gate_wait)
+        int e = 0;
+        SQ_HIP(hipMemcpy(&e, c->gate_err, sizeof e, hipMemcpyDeviceToHost));
+        if (e) return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange");
+    }
+    return SQ_OK;
 }
 
 int sq_slab(sq_ctx *c, long long *nz_local, long long *z0) {

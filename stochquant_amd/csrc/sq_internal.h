@@ -105,6 +105,16 @@ struct Phi4StepArgs {
     float *buf0, *buf1, *buf2;  // (named fields: a dynamic index would put the argument block in private memory)
     const FrameCtl *tctl;
     int tk;
+    // slab paths, gated launch (gate != nullptr; fused kernels): the first n_reg
+    // blocks are the usual chunks of the core range; the blocks after them are
+    // thin chunks (tzc planes, ntz per range) of the two rim ranges [tlo0, +tlen)
+    // and [thi0, +tlen), which read ghost planes: each first waits until
+    // *gate >= gate_seq -- stream B writes it behind the exchange -- so the
+    // core and the rims run in one launch without a stream hop
+    const unsigned int *gate;
+    unsigned int gate_seq;
+    int n_reg, tzc, tlen, tlo0, thi0, ntz;
+    int *gate_err;  // set when a wait gave up (kGateSpinMax)
 };
 constexpr int kStabSlots = 32;
 

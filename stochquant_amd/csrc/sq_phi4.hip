@@ -856,6 +856,60 @@ __device__ __forceinline__ void prio_by_progress(int q) {
     }
 }
 
+// A fused launch's block -> (y-band, x-segment, z-chunk).  Blocks are dealt
+// XCD-contiguously (consecutive ids round-robin over the 8 XCDs, so the
+// y-adjacent blocks sharing halo rows meet in one XCD's L2); a gated launch
+// (Phi4StepArgs::gate) appends its thin rim chunks after the n_reg core blocks,
+// so they are dispatched last, and maps them without the swizzle.
+struct TbBlock {
+    int yb, xs, z0, z1;
+    bool gated;
+};
+template <bool WIDE>
+__device__ __forceinline__ TbBlock tb_block(const Phi4StepArgs &A, int b, int nb) {
+    TbBlock t;
+    t.gated = A.gate != nullptr && b >= A.n_reg;
+    const int nbr = A.gate != nullptr ? A.n_reg : nb;
+    const int lb = t.gated ? b - A.n_reg : ((nbr & 7) == 0 ? (b & 7) * (nbr >> 3) + (b >> 3) : b);
+    t.yb = lb % A.nyg;
+    const int rest = lb / A.nyg;
+    t.xs = WIDE ? rest % A.nxseg : 0;
+    const int zk = WIDE ? rest / A.nxseg : rest;
+    if (t.gated) {
+        const int r0 = zk >= A.ntz ? A.thi0 : A.tlo0;
+        t.z0 = r0 + (zk % A.ntz) * A.tzc;
+        t.z1 = min(t.z0 + A.tzc, r0 + A.tlen);
+    } else {
+        const int r0 = A.zlo + (zk / A.nzr) * A.zstep;  // this chunk's range
+        t.z0 = r0 + (zk % A.nzr) * A.zc;
+        t.z1 = min(t.z0 + A.zc, r0 + A.zlen);
+    }
+    return t;
+}
+
+// A gated block waits for the exchange (its chunk reads ghost planes): one
+// thread polls the gate word with acquire loads at agent scope (no stream hop,
+// no L2 line kept: the word is fine-grained memory written behind the exchange
+// on stream B), the block follows through a barrier, and every wave acquires
+// before its first load of the ghost planes.  Bounded: after kGateSpinMax
+// polls the block gives up and flags gate_err (the host reports it), so a lost
+// exchange ends as an error, not a hung grid.
+constexpr unsigned int kGateSpinMax = 1u << 24;  // ~1 s of s_sleep 2
+__device__ __forceinline__ void tb_gate_wait(const Phi4StepArgs &A) {
+    if (threadIdx.x == 0) {
+        unsigned int n = 0;
+        while (__hip_atomic_load(A.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < A.gate_seq) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++n >= kGateSpinMax) {
+                if (A.gate_err) __hip_atomic_fetch_or(A.gate_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 constexpr int kTbRows = 8;
 constexpr int kTbWaves = kTbRows + 2;  // row waves; S > 1 adds the x-halo wave
 
@@ -1046,19 +1100,17 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
     // one XCD: the blocks sharing halo rows, edge columns and chunk-edge planes
-    // meet in that XCD's L2
-    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;
-    const int yb = lb % A.nyg, rest = lb / A.nyg;
-    const int xs = WIDE ? rest % A.nxseg : 0, zk = WIDE ? rest / A.nxseg : rest;
+    // meet in that XCD's L2 (tb_block)
+    const TbBlock tbk = tb_block<WIDE>(A, b, nb);
+    const int yb = tbk.yb, xs = tbk.xs;
     const int Lx = A.Lx, Ly = A.Ly;
     const int x0 = 256 * xs;
     TbCtx K;
     K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     K.lane = threadIdx.x & 63;
     K.outw = K.w >= 1 && K.w <= kTbRows;
-    const int r0 = A.zlo + (zk / A.nzr) * A.zstep;  // this chunk's range
-    K.z0 = r0 + (zk % A.nzr) * A.zc;
-    const int z1 = min(K.z0 + A.zc, r0 + A.zlen);
+    K.z0 = tbk.z0;
+    const int z1 = tbk.z1;
     K.z1 = z1;
     K.plane = (size_t)Lx * (size_t)Ly;
     K.pbytes = (uint32_t)(K.plane * sizeof(float));
@@ -1104,6 +1156,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     __shared__ float4 lds[3][kTbWaves][64];
     __shared__ float tx[WIDE ? 3 : 1][kTbWaves][2];
 
+    if (tbk.gated) tb_gate_wait(A);  // a rim chunk: its input's ghost planes come with the exchange
     TbIn I0, I1, I2;
     {
         const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
@@ -1318,18 +1371,16 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
-    const int lb = (nb & 7) == 0 ? (b & 7) * (nb >> 3) + (b >> 3) : b;  // as phi4_tb2_kernel
-    const int yb = lb % A.nyg, rest = lb / A.nyg;
-    const int xs = WIDE ? rest % A.nxseg : 0, zk = WIDE ? rest / A.nxseg : rest;
+    const TbBlock tbk = tb_block<WIDE>(A, b, nb);  // as phi4_tb2_kernel
+    const int yb = tbk.yb, xs = tbk.xs;
     const int Lx = A.Lx, Ly = A.Ly;
     const int x0 = 256 * xs;
     TbCtx K;
     K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     K.lane = threadIdx.x & 63;
     K.outw = K.w >= 1 && K.w <= kTbRows;
-    const int r0 = A.zlo + (zk / A.nzr) * A.zstep;
-    K.z0 = r0 + (zk % A.nzr) * A.zc;
-    K.z1 = min(K.z0 + A.zc, r0 + A.zlen);
+    K.z0 = tbk.z0;
+    K.z1 = tbk.z1;
     K.plane = (size_t)Lx * (size_t)Ly;
     K.pbytes = (uint32_t)(K.plane * sizeof(float));
     K.qplane = (uint32_t)(K.plane >> 2);
@@ -1380,6 +1431,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
     __shared__ float4 t_lds[2][kTbWaves][64];
     __shared__ float tx[WIDE ? 2 : 1][kTbWaves][2];
 
+    if (tbk.gated) tb_gate_wait(A);  // a rim chunk: its input's ghost planes come with the exchange
     // prologue: planes z0-2, z0-1, z0 (own rows), the rows beyond of z0-1 and
     // z0, edge sites / x-halo neighbours of plane z0-1; plane z0-1 published
     const __amdgpu_buffer_rsrc_t p0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
@@ -1825,8 +1877,16 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
     if (a.periodic ? (a.nz < 2 || a.zlo != 0 || a.zlen != a.nz || nr != 1)
                    : (a.zlo - 2 < -a.gz || last_end + 2 > a.nz + a.gz))  // input planes outside the buffer
         return hipErrorInvalidValue;
+    unsigned grid_n = (unsigned)a.nunits;
+    if (a.gate != nullptr) {  // core blocks + the thin gated rim chunks after them
+        if (a.n_reg != a.nunits || a.tzc < 1 || a.tlen < 1 || a.ntz != (a.tlen + a.tzc - 1) / a.tzc ||
+            a.tlo0 - 2 < -a.gz || a.tlo0 + a.tlen + 2 > a.nz + a.gz || a.thi0 - 2 < -a.gz ||
+            a.thi0 + a.tlen + 2 > a.nz + a.gz || a.periodic)
+            return hipErrorInvalidValue;
+        grid_n += (unsigned)(a.nxseg * a.nyg * 2 * a.ntz);
+    }
     const bool wide = a.nxseg > 1;
-    const dim3 grid((unsigned)a.nunits), block((kTbWaves + (wide ? 1 : 0)) * 64);
+    const dim3 grid(grid_n), block((kTbWaves + (wide ? 1 : 0)) * 64);
     const bool nz = a.sig != 0.0f;
     static const int wpe = getenv("SQ_TB2_WPE") ? atoi(getenv("SQ_TB2_WPE")) : 6;
     const bool fr = a.flag != nullptr;
