@@ -36,7 +36,7 @@ def main():
         rc = hip.hipSetDeviceFlags(ctypes.c_uint(fl))
         print(json.dumps({"hipSetDeviceFlags": a.flags, "rc": rc}), flush=True)
     import torch
-    from stochquant_amd import Phi4Lattice
+    from stochquant_amd import Phi4Lattice, _lib
     torch.cuda.set_device(0)
     L = a.size
     lat = Phi4Lattice((L, L, L), dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, device=0)
@@ -80,6 +80,12 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         rec("empty", (t1 - t0) * 1e6)
+        t0 = time.perf_counter()
+        lat.step(0)
+        rec("host_0", (time.perf_counter() - t0) * 1e6)
+        t0 = time.perf_counter()
+        _lib.load().sq_abi_version()
+        rec("host_abi", (time.perf_counter() - t0) * 1e6)
     out = {"flags": a.flags}
     out.update({k: round(statistics.median(v), 2) for k, v in res.items()})
     for K in (2, 20, 200):

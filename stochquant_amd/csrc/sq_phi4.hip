@@ -20,6 +20,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "sq_dpp.h"
 #include "sq_internal.h"
@@ -992,11 +993,28 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
 // compile-time constant).  WH: the padded buffers fit one 32-bit descriptor
 // each, and the plane is the buffer unit's scalar offset (one s_mul per plane
 // instead of the 64-bit descriptor base arithmetic).
-template <bool NZ, bool WIDE, bool FR, bool WH, int J>
+// P2 (256-site rows, raw steps; SQ_TB2_SYNC=p2p): no block barrier per plane.
+// Each wave publishes the last plane whose step-s row it wrote (prog[w],
+// workgroup-scope release) and, before overwriting a slot, waits until its one
+// or two row neighbours have published the plane before: they then have both
+// written the slot it reads next and finished reading the slot it overwrites
+// (three slots, a neighbour at most one plane behind).  A wave waits for two
+// waves, not for the block.
+__device__ __forceinline__ void tb_wait_nbrs(const int *prog, int w, int need) {
+    const int wl = w > 0 ? w - 1 : w + 1, wr = w < kTbWaves - 1 ? w + 1 : w - 1;
+    for (;;) {
+        const int a = __hip_atomic_load(&prog[wl], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int b = __hip_atomic_load(&prog[wr], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (__builtin_amdgcn_readfirstlane(min(a, b)) >= need) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <bool NZ, bool WIDE, bool FR, bool WH, int J, bool P2 = false>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, TbRun &R, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
-                                         FrameAcc &f2, float *bmx) {
+                                         FrameAcc &f2, float *bmx, int *prog = nullptr) {
     constexpr int sl = J, sp = (J + 2) % 3;  // slots of planes p and p-1
     __amdgpu_buffer_rsrc_t rs, rc;
     uint32_t ss = 0, sc = 0;
@@ -1040,6 +1058,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
                     (f32x4v){I2.row.x, I2.row.y, I2.row.z, I2.row.w},
                     reinterpret_cast<f32x4v *>(reinterpret_cast<char *>(A.snap) + (size_t)(p + 1) * K.pbytes + K.voff));
         }
+        if constexpr (P2) tb_wait_nbrs(prog, K.w, p - 1);
         lds[sl][K.w][K.lane] = T2;
     } else {
         // the x-halo wave: step s at its 16 sites of plane p
@@ -1052,7 +1071,11 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         const float t = tb_site(I1.row.x, xm, xp, ym, yp, I0.row.x, I2.row.x, xi, A, NZ);
         if (K.lane < 16) tx[sl][(K.lane & 7) + 1][K.lane >> 3] = t;
     }
-    __syncthreads();
+    if constexpr (P2) {
+        if (K.lane == 0) __hip_atomic_store(&prog[K.w], p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        __syncthreads();
+    }
     if (K.outw && p > K.z0) {
         const f32x4n xb = tb_noise<NZ>(A, R.qzm, K.qoff, K.slo1, K.shi1);
         const float4 up = lds[sp][K.w - 1][K.lane], dn = lds[sp][K.w + 1][K.lane];
@@ -1092,9 +1115,10 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 // 256-wide rows: 65 VGPRs, two 10-wave blocks per CU.  A 64-VGPR budget
 // (three blocks per CU) measured slower at every z-chunk
 // (profiles/r01/fuse2_sweep.log).
-template <bool NZ, bool WIDE, int WPE, bool FR, bool WH>
+template <bool NZ, bool WIDE, int WPE, bool FR, bool WH, bool P2 = false>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
+    static_assert(!P2 || (!WIDE && !FR), "neighbour sync: 256-site rows, raw steps");
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
@@ -1191,15 +1215,20 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     R.snext = (uint32_t)tb_pidx(A, K.z0) * K.pbytes;
     R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
     R.qzm = 0;  // plane z0-2: no step s+1 output there
+    __shared__ int prog[P2 ? kTbWaves : 1];  // P2: the last plane each row wave published
+    if constexpr (P2) {
+        if (threadIdx.x < kTbWaves) prog[threadIdx.x] = K.z0 - 2;
+        __syncthreads();
+    }
     // three-plane queues unrolled three ways so no rotation moves are emitted
     const PrioQ pq(K.z0, z1 - K.z0 + 2);
     for (int p = K.z0 - 1; p <= z1; p += 3) {
         if (A.prio) prio_by_progress(pq.q(p));
-        tb_plane<NZ, WIDE, FR, WH, 0>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2, bmx);
+        tb_plane<NZ, WIDE, FR, WH, 0, P2>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2, bmx, prog);
         if (p + 1 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 1>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2, bmx);
+        tb_plane<NZ, WIDE, FR, WH, 1, P2>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2, bmx, prog);
         if (p + 2 > z1) break;
-        tb_plane<NZ, WIDE, FR, WH, 2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2, bmx);
+        tb_plane<NZ, WIDE, FR, WH, 2, P2>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2, bmx, prog);
     }
     if constexpr (FR) frame_flush2(A, f1, f2, fk, fa);  // step s's records, then s+1's
     block_end_stamp(A);
@@ -1867,6 +1896,11 @@ hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_
 
 bool phi4_tb2_supported(int Lx, int Ly) { return Lx % 256 == 0 && Ly % kTbRows == 0; }
 
+static bool tb2_sync_p2p() {
+    const char *e = getenv("SQ_TB2_SYNC");  // read per launch (tests switch it within a process)
+    return e != nullptr && strcmp(e, "p2p") == 0;
+}
+
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0 || a.nxseg != a.Lx / 256 || a.nyg != a.Ly / kTbRows ||
         a.nzr < 1 || a.nzc % a.nzr != 0 || a.nunits != a.nxseg * a.nyg * a.nzc || a.zlen < 1 ||
@@ -1913,6 +1947,11 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
                   // fit a CU only when the second one's waves land 2-2-3-3 against the first's
                   // 3-3-2-2; frame launches 53 vs 45 us at 256^3)
         fn = nz ? SQ_TB2F(true, false, 6, true) : SQ_TB2F(false, false, 6, true);
+    else if (!pipe && tb2_sync_p2p())  // SQ_TB2_SYNC=p2p: neighbour progress words instead of the barrier
+        fn = nz ? (wh ? (const void *)&phi4_tb2_kernel<true, false, 1, false, true, true>
+                      : (const void *)&phi4_tb2_kernel<true, false, 1, false, false, true>)
+                : (wh ? (const void *)&phi4_tb2_kernel<false, false, 1, false, true, true>
+                      : (const void *)&phi4_tb2_kernel<false, false, 1, false, false, true>);
     else
         fn = nz ? SQ_TB2F(true, false, 1, false) : SQ_TB2F(false, false, 1, false);
 #undef SQ_TB2

@@ -863,6 +863,30 @@ def test_frame_launches_equal_raw_steps_repeated(gpu, oracle_mod, monkeypatch, p
         assert np.array_equal(run(True), ref)
 
 
+@pytest.mark.parametrize("shape,kw", [((256, 16, 24), {}), ((256, 64, 64), {}),
+                                      ((256, 32, 40), {"comm": "loopback", "nslabs": 2})])
+def test_neighbour_sync_equals_block_barrier(gpu, monkeypatch, shape, kw):
+    """SQ_TB2_SYNC=p2p (row waves wait for their two neighbours' progress words
+    instead of a block barrier per plane) gives the barrier kernel's field bit
+    for bit, over repeated runs: a missing wait would read a neighbour's row of
+    the wrong plane in some runs.  Plain and slab (ghost-zone) contexts."""
+    monkeypatch.setenv("SQ_TB2_PIPE", "0")
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    rng = np.random.default_rng(91)
+    phi0 = (0.9 * rng.standard_normal((shape[2], shape[1], shape[0]))).astype(np.float32)
+
+    def run(sync):
+        monkeypatch.setenv("SQ_TB2_SYNC", sync)
+        with _lat(shape, loops=8, dtau=0.01, m2=0.5, lam=1.0, seed=91, **kw) as L:
+            L.upload(phi0)
+            L.step(8)
+            return L.download()
+
+    ref = run("barrier")
+    for _ in range(4):
+        assert np.array_equal(run("p2p"), ref)
+
+
 RUN_FRAMES_CASES = [((256, 16, 16), 6, {}), ((256, 8, 12), 5, {}), ((64, 16, 8), 6, {}),
                     ((512, 8, 6), 4, {}), ((256, 8, 12), 6, {"comm": "loopback", "nslabs": 3})]
 
