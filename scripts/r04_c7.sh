@@ -26,3 +26,5 @@ for r in 1 2; do for g in 0 1; do
   SQ_SLAB_GATE=$g timeout -k 10 180 python3 bench.py --comm p2p --steps 2000 --warmup 200 --settle-ms 800 --no-cpu-baseline --no-c3 --no-c1 --no-check > $O/p2p_g${g}_$r.log 2>&1; rc=$?; fatal $rc p2p; [ $rc -eq 0 ] || { tail $O/p2p_g${g}_$r.log; exit 3; }
   echo "p2p gate=$g run=$r $(grep -o '"ms_per_step": [0-9.]*' $O/p2p_g${g}_$r.log)"
 done; done
+# (4) the neighbour-sync A/B (scripts/r04_c8.sh) when the call has time left
+if [ $SECONDS -lt 650 ]; then bash scripts/r04_c8.sh ${1:-r04_c7}/p2sync; rc=$?; echo "p2sync rc=$rc"; fi

@@ -993,7 +993,7 @@ __device__ __forceinline__ float tb_site(float phi, float xm, float xp, float ym
 // compile-time constant).  WH: the padded buffers fit one 32-bit descriptor
 // each, and the plane is the buffer unit's scalar offset (one s_mul per plane
 // instead of the 64-bit descriptor base arithmetic).
-// P2 (256-site rows, raw steps; SQ_TB2_SYNC=p2p): no block barrier per plane.
+// P2 (256-site rows; SQ_TB2_SYNC=p2p): no block barrier per plane.
 // Each wave publishes the last plane whose step-s row it wrote (prog[w],
 // workgroup-scope release) and, before overwriting a slot, waits until its one
 // or two row neighbours have published the plane before: they then have both
@@ -1118,7 +1118,7 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
 template <bool NZ, bool WIDE, int WPE, bool FR, bool WH, bool P2 = false>
 __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArgs A0) {
-    static_assert(!P2 || (!WIDE && !FR), "neighbour sync: 256-site rows, raw steps");
+    static_assert(!P2 || !WIDE, "neighbour sync: 256-site rows");
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
     if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
@@ -1943,6 +1943,11 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
         fn = nz ? SQ_TB2(true, true, 6) : SQ_TB2(false, true, 6);
     else if (wide)
         fn = nz ? SQ_TB2(true, true, 1) : SQ_TB2(false, true, 1);
+    else if (fr && !pipe && tb2_sync_p2p())
+        fn = nz ? (wh ? (const void *)&phi4_tb2_kernel<true, false, 6, true, true, true>
+                      : (const void *)&phi4_tb2_kernel<true, false, 6, true, false, true>)
+                : (wh ? (const void *)&phi4_tb2_kernel<false, false, 6, true, true, true>
+                      : (const void *)&phi4_tb2_kernel<false, false, 6, true, false, true>);
     else if (fr)  // 78 VGPRs (unconstrained: 81, 88 allocated, 5 waves per SIMD: two 10-wave blocks
                   // fit a CU only when the second one's waves land 2-2-3-3 against the first's
                   // 3-3-2-2; frame launches 53 vs 45 us at 256^3)

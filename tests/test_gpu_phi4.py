@@ -875,16 +875,24 @@ def test_neighbour_sync_equals_block_barrier(gpu, monkeypatch, shape, kw):
     rng = np.random.default_rng(91)
     phi0 = (0.9 * rng.standard_normal((shape[2], shape[1], shape[0]))).astype(np.float32)
 
-    def run(sync):
+    def run(sync, frame):
         monkeypatch.setenv("SQ_TB2_SYNC", sync)
         with _lat(shape, loops=8, dtau=0.01, m2=0.5, lam=1.0, seed=91, **kw) as L:
             L.upload(phi0)
+            if frame:  # the frame kernels (records, fold) under either sync
+                ok = L.run_frame()
+                return L.download(), ok, L.dtau
             L.step(8)
             return L.download()
 
-    ref = run("barrier")
+    ref = run("barrier", False)
     for _ in range(4):
-        assert np.array_equal(run("p2p"), ref)
+        assert np.array_equal(run("p2p", False), ref)
+    if not kw:
+        fref = run("barrier", True)
+        for _ in range(2):
+            got = run("p2p", True)
+            assert np.array_equal(got[0], fref[0]) and got[1:] == fref[1:]
 
 
 RUN_FRAMES_CASES = [((256, 16, 16), 6, {}), ((256, 8, 12), 5, {}), ((64, 16, 8), 6, {}),
