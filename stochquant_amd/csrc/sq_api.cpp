@@ -242,7 +242,7 @@ struct sq_ctx {
     // its last blocks for a second round (core pair 43-45 us vs 33)
     int tb_blocks_xchg = 416;
     bool beside_xchg = false;       // the launch being issued runs beside an exchange
-    // gated pair 0 (SQ_SLAB_GATE, default on): K = 1 blocks run the core pair and
+    // gated pair 0 (SQ_SLAB_GATE=1; default off, slower: DESIGN.md §8.0): K = 1 blocks run the core pair and
     // the rim pair as ONE launch whose thin rim chunks wait in-kernel for the
     // exchange (Phi4StepArgs::gate), no WAIT_EXCHANGE hop and no small rim grid
     bool slab_gate = false;
@@ -1243,7 +1243,7 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipMalloc(&c->gate_err, sizeof(int)));
         SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
         const char *e = getenv("SQ_SLAB_GATE");
-        c->slab_gate = e ? atoi(e) != 0 : true;
+        c->slab_gate = e ? atoi(e) != 0 : false;  // off: its spinning rim blocks hold the CU slots the exchange needs
     }
     if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
         // fine-grained device memory: the words are written by the peers'

@@ -411,14 +411,17 @@ def test_fused_two_step_deep_halo_bitwise(gpu, oracle_mod, monkeypatch, shape, g
         assert np.array_equal(mono, L.download())
 
 
-@pytest.mark.parametrize("core_pairs,rims_b", [("0", "0"), ("1", "1"), ("2", "0"), ("2", "1"), ("4", "0"),
-                                                ("4", "1"), ("8", "1")])
-def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs, rims_b):
+@pytest.mark.parametrize("core_pairs,rims_b,gate", [("0", "0", "0"), ("1", "0", "0"), ("1", "0", "1"), ("1", "1", "0"),
+                                                     ("2", "0", "0"), ("2", "1", "0"), ("4", "0", "0"),
+                                                     ("4", "1", "0"), ("8", "1", "0")])
+def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs, rims_b, gate):
     """K fused core pairs before the exchange wait (K = 0: none, the first
     pair waits for the exchange), their rims after it on stream A or on the
-    exchange stream (the C4 overlap for slow links): RCCL self-exchange, P2P
-    self-exchange and loopback slabs == the single-slab run, bit for bit,
-    over full and partial blocks."""
+    exchange stream (the C4 overlap for slow links), K = 1 also as the gated
+    launch (SQ_SLAB_GATE=1: rim chunks wait in-kernel for the exchange): RCCL
+    self-exchange, P2P self-exchange and loopback slabs == the single-slab
+    run, bit for bit, over full and partial blocks."""
+    monkeypatch.setenv("SQ_SLAB_GATE", gate)
     from stochquant_amd import unique_id
     shape = (256, 16, 96)
     phi0 = _init(oracle_mod, shape)
