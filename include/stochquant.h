@@ -266,6 +266,10 @@ int sq_sync(sq_ctx *ctx);
  * (cap >= blocks of the launch); *nblocks = blocks.  A measurement hook for
  * the launch's ramp, tail and busy fraction (bench.py roofline). */
 int sq_phi4_block_stamps(sq_ctx *ctx, unsigned long long *out, int cap, int *nblocks);
+/* The same launch's shader-clock counter (s_memtime) at each block's start and
+ * end, out[2b], out[2b+1]: with sq_phi4_block_stamps, the clock the launch ran
+ * at under the chip's power management (bench.py clock_MHz_measured). */
+int sq_phi4_block_clocks(sq_ctx *ctx, unsigned long long *out, int cap, int *nblocks);
 
 /* RCCL bootstrap: rank 0 creates the id, the caller distributes it (e.g. via
  * torch.distributed) into sq_params.comm_id of every rank. */

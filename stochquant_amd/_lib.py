@@ -138,6 +138,7 @@ SIGNATURES = {
     "sq_perf_reset": (ctypes.c_int, [_P]),
     "sq_sync": (ctypes.c_int, [_P]),
     "sq_phi4_block_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, _I]),
+    "sq_phi4_block_clocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, _I]),
     "sq_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ubyte)]),
     "sq_p2p_handle": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ubyte)]),
     "sq_p2p_connect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ubyte), ctypes.c_int]),

@@ -2266,7 +2266,7 @@ int sq_phi4_block_stamps(sq_ctx *c, unsigned long long *out, int cap, int *nbloc
     if (c->stamps_cap < need) {
         (void)hipFree(c->dstamps);
         c->stamps_cap = 0;
-        SQ_HIP(hipMalloc(&c->dstamps, 2 * sizeof(unsigned long long) * (size_t)need));
+        SQ_HIP(hipMalloc(&c->dstamps, 4 * sizeof(unsigned long long) * (size_t)need));  // + the shader clock
         c->stamps_cap = need;
     }
     c->stamps_next = c->dstamps;
@@ -2277,6 +2277,20 @@ int sq_phi4_block_stamps(sq_ctx *c, unsigned long long *out, int cap, int *nbloc
     if (c->stamps_blocks > cap) return fail(SQ_E_ARG, "cap smaller than the launch's blocks");
     SQ_HIP(hipMemcpyAsync(out, c->dstamps, 2 * sizeof(unsigned long long) * (size_t)c->stamps_blocks,
                           hipMemcpyDeviceToHost, c->slabs[0].sA));
+    SQ_HIP(hipStreamSynchronize(c->slabs[0].sA));
+    *nblocks = c->stamps_blocks;
+    return SQ_OK;
+}
+
+int sq_phi4_block_clocks(sq_ctx *c, unsigned long long *out, int cap, int *nblocks) {
+    if (!c || !out || !nblocks || cap < 1) return fail(SQ_E_ARG, "null argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (c->dstamps == nullptr || c->stamps_blocks < 1) return fail(SQ_E_STATE, "no sq_phi4_block_stamps launch yet");
+    if (c->stamps_blocks > cap) return fail(SQ_E_ARG, "cap smaller than the launch's blocks");
+    DeviceGuard g(c->dev);
+    const size_t n = 2 * (size_t)c->stamps_blocks;  // written behind the 2 x blocks constant-clock stamps
+    SQ_HIP(hipMemcpyAsync(out, c->dstamps + n, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost,
+                          c->slabs[0].sA));
     SQ_HIP(hipStreamSynchronize(c->slabs[0].sA));
     *nblocks = c->stamps_blocks;
     return SQ_OK;

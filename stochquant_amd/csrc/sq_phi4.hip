@@ -830,11 +830,20 @@ __global__ __launch_bounds__(256) void phi4_step_kernel(const Phi4StepArgs A0) {
 // gets the higher priority: 3 in its first quarter of planes, down to 0 in
 // its last (4 levels beat 2: 3 then 0 by halves, 512^3 139-140 vs 136-137
 // us/step).  q = quarter (0..3), wave-uniform.
-// Block stamps (Phi4StepArgs::stamps): the end, once every wave is done.
+// Block stamps (Phi4StepArgs::stamps): [2b, 2b+1] the constant 100 MHz clock
+// (s_memrealtime) at the block's start and end, [2 nb + 2b, 2 nb + 2b + 1] the
+// shader-clock counter (s_memtime) at the same two points: their ratio is the
+// clock the block ran at (the chip's power management moves it; sq_phi4_block_clocks).
+__device__ __forceinline__ void block_stamp(const Phi4StepArgs &A, int at) {
+    const unsigned long long rt = __builtin_amdgcn_s_memrealtime(), ct = __builtin_amdgcn_s_memtime();
+    A.stamps[2 * blockIdx.x + at] = rt;
+    A.stamps[2 * gridDim.x + 2 * blockIdx.x + at] = ct;
+}
+// the end, once every wave is done
 __device__ __forceinline__ void block_end_stamp(const Phi4StepArgs &A) {
     if (A.stamps == nullptr) return;
     __syncthreads();
-    if (threadIdx.x == 0) A.stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) block_stamp(A, 1);
 }
 
 // The march's quarter boundaries: plane p (p = z0-1 .. z1) is in quarter
@@ -1121,7 +1130,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     static_assert(!P2 || !WIDE, "neighbour sync: 256-site rows");
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
-    if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
+    if (A.stamps != nullptr && threadIdx.x == 0) block_stamp(A, 0);
     // y-bands fastest, then x-segments, then z-chunks, consecutive blocks on
     // one XCD: the blocks sharing halo rows, edge columns and chunk-edge planes
     // meet in that XCD's L2 (tb_block)
@@ -1399,7 +1408,7 @@ __global__ __launch_bounds__((kTbWaves + (WIDE ? 1 : 0)) * 64)
 __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepArgs A0) {
     const Phi4StepArgs A = frame_args<FR>(A0);
     const int nb = gridDim.x, b = blockIdx.x;
-    if (A.stamps != nullptr && threadIdx.x == 0) A.stamps[2 * b] = __builtin_amdgcn_s_memrealtime();
+    if (A.stamps != nullptr && threadIdx.x == 0) block_stamp(A, 0);
     const TbBlock tbk = tb_block<WIDE>(A, b, nb);  // as phi4_tb2_kernel
     const int yb = tbk.yb, xs = tbk.xs;
     const int Lx = A.Lx, Ly = A.Ly;

@@ -319,6 +319,16 @@ class Phi4Lattice(_Ctx):
         a = a[:2 * nb.value].astype(np.int64)
         return a[0::2], a[1::2]
 
+    def block_clocks(self, cap=1 << 16):
+        """The last block_stamps launch's shader-clock counter (s_memtime) at each
+        block's start and end: (start, end) int64 arrays in shader cycles."""
+        a = np.zeros(2 * cap, dtype=np.uint64)
+        nb = ctypes.c_int()
+        _lib.call("sq_phi4_block_clocks", self._h, a.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), int(cap),
+                  ctypes.byref(nb))
+        a = a[:2 * nb.value].astype(np.int64)
+        return a[0::2], a[1::2]
+
     def set_stability(self, T, V):
         _lib.call("sq_phi4_set_stability", self._h, float(T), float(V))
 

@@ -982,5 +982,12 @@ def test_block_stamps_are_two_steps(gpu, oracle_mod):
         st, en = L.block_stamps()
         R.step(2)
         assert len(st) == len(en) > 0 and (en >= st).all() and (st > 0).all()
+        # the same blocks' shader-clock counters: a clock between 100 MHz and 3 GHz
+        cs, ce = L.block_clocks()
+        assert len(cs) == len(st) and (ce >= cs).all()
+        ok = en - st > 100  # blocks that ran >= 1 us of the 100 MHz clock
+        assert ok.any()
+        mhz = np.median((ce[ok] - cs[ok]) / (en[ok] - st[ok])) * 100.0
+        assert 100.0 <= mhz <= 3000.0, mhz
         assert L.step_counter == R.step_counter == 3
         assert np.array_equal(L.download(), R.download())
