@@ -312,13 +312,21 @@ __device__ __forceinline__ void frame_flush2(const Phi4StepArgs &A, const FrameA
     const bool bad = f1.am >= A.clampv || f2.am >= A.clampv;
     if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(A.flag, 1);
     if (A.st_md == nullptr) return;  // a kernel argument: every thread returns here or none
-    const unsigned long long k1 = dpp_all_max_u64(((uint64_t)ord_f32(f1.m) << 32) | __float_as_uint(f1.d));
-    const unsigned long long k2 = dpp_all_max_u64(((uint64_t)ord_f32(f2.m) << 32) | __float_as_uint(f2.d));
+    // The wave's key: f.mw is the DPP maximum of the lanes' m at their last
+    // per-site update (frame_sites), possibly raised since to the block's
+    // threshold, so only lanes whose m reaches it can hold the wave's maximum
+    // key -- usually one lane -- and only they post it (an exec-masked LDS
+    // atomic instead of two 64-bit DPP scans per wave, ~60 VALU).  No lane
+    // qualifies when the block's threshold passed the wave's maximum: another
+    // wave's lanes hold a key at least as large.  Waves without sites in a
+    // record (m = mw = -inf) post nothing.
+    if (f1.m >= f1.mw && f1.mw > -__builtin_inff())
+        atomicMax(&fk[0], ((uint64_t)ord_f32(f1.m) << 32) | __float_as_uint(f1.d));
+    if (f2.m >= f2.mw && f2.mw > -__builtin_inff())
+        atomicMax(&fk[1], ((uint64_t)ord_f32(f2.m) << 32) | __float_as_uint(f2.d));
     const uint32_t a1 = (uint32_t)dpp_all_max_i((int)__float_as_uint(fminf(f1.am, A.clampv)));
     const uint32_t a2 = (uint32_t)dpp_all_max_i((int)__float_as_uint(fminf(f2.am, A.clampv)));
     if ((threadIdx.x & 63) == 0) {
-        atomicMax(&fk[0], k1);
-        atomicMax(&fk[1], k2);
         atomicMax(&fa[0], a1);
         atomicMax(&fa[1], a2);
     }
