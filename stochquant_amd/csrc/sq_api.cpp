@@ -242,6 +242,12 @@ struct sq_ctx {
     // its last blocks for a second round (core pair 43-45 us vs 33)
     int tb_blocks_xchg = 416;
     bool beside_xchg = false;       // the launch being issued runs beside an exchange
+    // EDGES_DONE as the stop event of the pair before it (SQ_EDGES_STOPEV=1):
+    // hipExtLaunchKernel binds the event to the dispatch itself instead of a
+    // marker packet behind it on stream A (each marker leaves a 5-7 us bubble)
+    bool edges_stopev = false;
+    hipEvent_t stop_next = nullptr;  // the next fused launch's stop event
+    bool stop_used = false;          // ... which EDGES_DONE then need not record
     // gated pair 0 (SQ_SLAB_GATE=1; default off, slower: DESIGN.md §8.0): K = 1 blocks run the core pair and
     // the rim pair as ONE launch whose thin rim chunks wait in-kernel for the
     // exchange (Phi4StepArgs::gate), no WAIT_EXCHANGE hop and no small rim grid
@@ -569,7 +575,14 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
         if (a.nunits > c->stamps_cap) return fail(SQ_E_STATE, "block stamps: more blocks than stamp slots");
         c->stamps_blocks = a.nunits;
     }
-    SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    hipEvent_t stop = c->stop_next;
+    c->stop_next = nullptr;
+    if (e == nullptr && stop != nullptr) {
+        SQ_HIP(sq::phi4_tb2_launch(a, st, nullptr, stop));
+        c->stop_used = true;
+    } else {
+        SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    }
     c->perf.kernel_launches += 1;
     c->perf.fused_steps += 2;
     return SQ_OK;
@@ -870,12 +883,17 @@ int phi4_block(sq_ctx *c, int g) {
                 const bool first = !timed[gi];  // it carries the group's timing
                 timed[gi] = 1;
                 c->step = step0 + (unsigned long long)op.step;
+                c->stop_used = false;
+                if (c->edges_stopev && op.kind == SQ_OP_PAIR && oi + 1 < ops.size() &&
+                    ops[oi + 1].kind == SQ_OP_EDGES_DONE && ops[oi + 1].stream == op.stream)
+                    c->stop_next = s.evE;  // phi4_tb2_range binds it to the launch (stop_used)
                 if (op.kind == SQ_OP_PAIR)
                     rc = phi4_tb2_range(c, s, in, st, op.lo, op.hi, op.lo2, op.hi2, 0, first);
                 else if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
                     rc = phi4_launch_range(c, s, in, st, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
                 else
                     rc = phi4_launch_span(c, s, in, st, op.lo, op.hi, first);
+                c->stop_next = nullptr;  // an empty range launched nothing: EDGES_DONE records
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
                 if (op.stream != kB) xchg_live = false;
                 if (op.stream != kB) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));  // B: ordered behind its exchange
@@ -887,7 +905,8 @@ int phi4_block(sq_ctx *c, int g) {
                 SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));
             } else if (op.kind == SQ_OP_EDGES_DONE) {
                 xchg_live = true;
-                SQ_HIP(hipEventRecord(s.evE, st));
+                if (!c->stop_used) SQ_HIP(hipEventRecord(s.evE, st));  // else bound to the pair before
+                c->stop_used = false;
             } else if (op.kind == SQ_OP_SIGNAL || op.kind == SQ_OP_WAIT) {
                 if (op.lo < 0 || op.lo >= kPlanSlots) return fail(SQ_E_STATE, "block op event slot out of range");
                 if (op.kind == SQ_OP_SIGNAL)
@@ -1328,6 +1347,7 @@ int create_phi4(sq_ctx *c) {
         // 448 19.02 / 19.32, 416 18.89 / 19.24; SQ_XCHG_BLOCKS pins the target
         c->tb_blocks_xchg = std::max(1, c->tb_blocks - 96);
         if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
+        if (const char *e = getenv("SQ_EDGES_STOPEV")) c->edges_stopev = atoi(e) != 0;
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;

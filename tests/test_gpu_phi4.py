@@ -411,17 +411,21 @@ def test_fused_two_step_deep_halo_bitwise(gpu, oracle_mod, monkeypatch, shape, g
         assert np.array_equal(mono, L.download())
 
 
-@pytest.mark.parametrize("core_pairs,rims_b,gate", [("0", "0", "0"), ("1", "0", "0"), ("1", "0", "1"), ("1", "1", "0"),
-                                                     ("2", "0", "0"), ("2", "1", "0"), ("4", "0", "0"),
-                                                     ("4", "1", "0"), ("8", "1", "0")])
-def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs, rims_b, gate):
+@pytest.mark.parametrize("core_pairs,rims_b,gate,stopev", [("0", "0", "0", "0"), ("1", "0", "0", "0"), ("1", "0", "1", "0"),
+                                                            ("1", "0", "0", "1"), ("0", "0", "0", "1"),
+                                                            ("1", "1", "0", "0"), ("2", "0", "0", "0"),
+                                                            ("2", "1", "0", "0"), ("4", "0", "0", "0"),
+                                                            ("4", "1", "0", "1"), ("8", "1", "0", "0")])
+def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, core_pairs, rims_b, gate, stopev):
     """K fused core pairs before the exchange wait (K = 0: none, the first
     pair waits for the exchange), their rims after it on stream A or on the
     exchange stream (the C4 overlap for slow links), K = 1 also as the gated
     launch (SQ_SLAB_GATE=1: rim chunks wait in-kernel for the exchange): RCCL
     self-exchange, P2P self-exchange and loopback slabs == the single-slab
-    run, bit for bit, over full and partial blocks."""
+    run, bit for bit, over full and partial blocks; EDGES_DONE as a marker or
+    as the stop event of the pair before it (SQ_EDGES_STOPEV)."""
     monkeypatch.setenv("SQ_SLAB_GATE", gate)
+    monkeypatch.setenv("SQ_EDGES_STOPEV", stopev)
     from stochquant_amd import unique_id
     shape = (256, 16, 96)
     phi0 = _init(oracle_mod, shape)
