@@ -22,3 +22,12 @@ f=$(find $O/ftr -name '*kernel_trace.csv' | head -1)
 python3 scripts/frame_timeline.py "$f" > $O/frame_timeline.txt 2>&1; cat $O/frame_timeline.txt
 cp $(find $O/ftr -name '*kernel_stats.csv' | head -1) $O/rows_f_kernel_stats.csv
 find $O/ftr -name '*kernel_trace.csv' -delete
+# EDGES_DONE as the stop event of the pair before it (SQ_EDGES_STOPEV)
+timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_phi4.py \
+  -k "core_pairs_ahead" > $O/slab_tests.log 2>&1 || { tail -30 $O/slab_tests.log; exit 4; }
+tail -1 $O/slab_tests.log
+S="--steps 2000 --warmup 200 --settle-ms 800 --no-cpu-baseline --no-c3 --no-c1 --no-check"
+for r in 1 2; do for t in rccl p2p; do for v in 0 1; do
+  SQ_EDGES_STOPEV=$v timeout -k 10 180 python3 bench.py --comm $t $S > $O/slab_${t}_ev${v}_$r.log 2>&1 || { tail $O/slab_${t}_ev${v}_$r.log; exit 5; }
+  echo "$t stopev=$v run=$r $(grep -o '"ms_per_step": [0-9.]*' $O/slab_${t}_ev${v}_$r.log)"
+done; done; done
