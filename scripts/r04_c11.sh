@@ -11,7 +11,7 @@ timeout -k 10 400 python3 -u -m pytest -x -q --timeout 120 --timeout-method thre
   -k "frame or stab or guard or snapshot or checkpoint or record" > $O/frame_tests.log 2>&1 || { tail -30 $O/frame_tests.log; exit 1; }
 tail -1 $O/frame_tests.log
 BASE=stochquant_amd/lib/ab/libstochquant_base.so
-for r in 1 2 3; do for v in base new; do
+for r in 1 2 3 4; do for v in base new; do
   if [ $v = base ]; then export SQ_LIB=$BASE; else unset SQ_LIB; fi
   timeout -k 10 200 python3 -u scripts/bench_rows_f.py > $O/rows_f_${v}_$r.log 2>&1 || { tail $O/rows_f_${v}_$r.log; exit 2; }
   echo "frames $v run=$r $(grep -h 'f1' $O/rows_f_${v}_$r.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["raw_steps_us"], d["batch_frame_us"], d["frame_us"])')"
@@ -23,6 +23,7 @@ python3 scripts/frame_timeline.py "$f" > $O/frame_timeline.txt 2>&1; cat $O/fram
 cp $(find $O/ftr -name '*kernel_stats.csv' | head -1) $O/rows_f_kernel_stats.csv
 find $O/ftr -name '*kernel_trace.csv' -delete
 # EDGES_DONE as the stop event of the pair before it (SQ_EDGES_STOPEV)
+[ -n "$SKIP_SLAB" ] && exit 0
 timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_phi4.py \
   -k "core_pairs_ahead" > $O/slab_tests.log 2>&1 || { tail -30 $O/slab_tests.log; exit 4; }
 tail -1 $O/slab_tests.log
