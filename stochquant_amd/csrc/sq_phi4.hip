@@ -1333,7 +1333,7 @@ __device__ __forceinline__ void tp_row(const Phi4StepArgs &A, const TbCtx &K, Tp
     in_lds[sn][K.w + 1][K.lane] = I[ip];
     if (xrow) in_lds[sn][xslot][K.lane] = X[sn];
     if constexpr (FR) {  // each output row's input at its owned planes, once, nontemporal
-        const bool sv = A.snap != nullptr && K.outw && k + 1 >= K.z0 && k + 1 < K.z1;
+        const bool sv = K.snapw != 0 && k + 1 >= K.z0 && k + 1 < K.z1;
         bstore4<2>(plane_rsrc(A.snap, k + 1, K.plane, K.pbytes), sv ? K.voff : kTpOob, I[ip]);
     }
     // 3. A: step s at plane k
@@ -1431,6 +1431,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
     K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     K.lane = threadIdx.x & 63;
     K.outw = K.w >= 1 && K.w <= kTbRows;
+    K.snapw = __builtin_amdgcn_readfirstlane((FR && A.snap != nullptr && K.outw) ? 1 : 0);
     K.z0 = tbk.z0;
     K.z1 = tbk.z1;
     K.plane = (size_t)Lx * (size_t)Ly;
