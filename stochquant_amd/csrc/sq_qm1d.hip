@@ -751,7 +751,10 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             grid_barrier(bar, (unsigned int)(j + 1));
         else
             grid.sync();
-        __threadfence();
+        // acquire only: every block's writes before the barrier were released by
+        // its thread 0 (after the block's __syncthreads) -- a full __threadfence
+        // here made every wave write back the L2 again each step
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         if (j < A.loops) {  // step j+1's neighbours and f[mid], stored by their owners before the barrier
             if (own > 0) {
                 fL = i0 > 0 ? fout[i0 - 1] : 0.;
