@@ -645,18 +645,6 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     int stable = 1, steps = 0;
     const double *fin = A.f;
     double *fout = A.nf;
-    // the field a step reads: the thread's own sites stay in registers from the
-    // step that computed them (the same values it stored); only the two
-    // neighbouring sites and f[mid] come from global memory, loaded right after
-    // the barrier together with the scan's words, so their round trip overlaps
-    // the scan's instead of following it
-    double fc[kGridK];
-#pragma unroll
-    for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
-    double fL = (own > 0 && i0 > 0) ? fin[i0 - 1] : 0.;
-    double fR = (own > 0 && i0 + own < N) ? fin[i0 + own] : 0.;
-    double fmid = fin[mid];
-    const UDiv da2 = udiv_prep(a2);
     for (int j = 0; j <= A.loops; ++j) {
         const int par = j & 1;
         double X[kGridK];
@@ -665,42 +653,16 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             // 1. site updates of step j
             const unsigned long long step = A.tick + (unsigned long long)j;
             const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-            const double Xm = fmid + xcl((double)mid * a, om, pot);
+            const double Xm = fin[mid] + xcl((double)mid * a, om, pot);
             const double den = (double)(A.runs + j + 1);
             double lmaxX = -INFINITY, lmaxA = -INFINITY;
             if (own > 0) {
-                // numerators first, then every quotient of the step by the
-                // shared-divisor form (udiv_step: exact, one wave-uniform
-                // fallback branch), as qm1d_frame_wave -- three fp64 divisions
-                // per site were most of the step's dependent latency
-                const UDiv dden = udiv_prep(den);
-                double nA[kGridK], qA[kGridK], nM2[2 * kGridK], qM2[2 * kGridK], xcv[kGridK];
-                bool bad = false;
-#pragma unroll
-                for (int k = 0; k < kGridK; ++k) {
-                    nA[k] = nM2[k] = nM2[kGridK + k] = xcv[k] = 0.;
-                    if (k >= own) continue;
-                    const int i = i0 + k;
-                    const double fi = fc[k];
-                    const double fr = (k + 1 < own) ? fc[k + 1] : fR;
-                    const double prev_old = k == 0 ? fL : fc[k - 1];
-                    const double xc = xcl((double)i * a, om, pot);
-                    xcv[k] = xc;
-                    if (i == 0)
-                        nA[k] = kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi);
-                    else if (i == N - 1)
-                        nA[k] = kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi);
-                    else
-                        nA[k] = kM * h * (fr + prev_old - 2 * fi);
-                    const double Xi = fi + xc;  // running means from the OLD field
-                    nM2[k] = Xi * Xm - nxx0[k];
-                    nM2[kGridK + k] = Xi - nx[k];
-                    bad = bad || !(udiv_range(nA[k]) && udiv_range(nM2[k]) && udiv_range(nM2[kGridK + k]));
-                }
-                udiv_step<kGridK, true>(nA, da2, qA, bad);
-                udiv_step<2 * kGridK, true>(nM2, dden, qM2, bad);
                 f32x4n nq = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
-                double fn[kGridK];
+                double fc[kGridK];
+#pragma unroll
+                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
+                const double fL = i0 > 0 ? fin[i0 - 1] : 0.;
+                const double fR = i0 + own < N ? fin[i0 + own] : 0.;
 #pragma unroll
                 for (int k = 0; k < kGridK; ++k) {
                     if (k >= own) break;
@@ -710,9 +672,19 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                         nq = normals4((unsigned long long)(i >> 2), kStreamField, slo, shi, A.k0, A.k1);
                     const float xi = c == 0 ? nq.a : c == 1 ? nq.b : c == 2 ? nq.c : nq.d;
                     const double fi = fc[k];
-                    const double xc = xcv[k];
+                    const double fr = (k + 1 < own) ? fc[k + 1] : fR;
+                    const double prev_old = k == 0 ? fL : fc[k - 1];
+                    const double xc = xcl((double)i * a, om, pot);
                     const double dw = A.sig * (double)xi;
-                    double v = fi + qA[k] - ddpot(xc, pot) * fi * h + dw;
+                    double v;
+                    if (i == 0)
+                        v = fi + kM * h * (fr + (-kEta) - xcl(-1. * a, om, pot) - 2 * fi) / a2 -
+                            ddpot(xc, pot) * fi * h + dw;
+                    else if (i == N - 1)
+                        v = fi + kM * h * (prev_old + kEta - xcl((double)N * a, om, pot) - 2 * fi) / a2 -
+                            ddpot(xc, pot) * fi * h + dw;
+                    else
+                        v = fi + kM * h * (fr + prev_old - 2 * fi) / a2 - ddpot(xc, pot) * fi * h + dw;
                     if (v > 1000) v = 1000;
                     if (v < -1000) v = -1000;
                     if (v != v) v = 1000;
@@ -720,15 +692,12 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     D[k] = absol(v - fi - dw);
                     lmaxX = fmax(lmaxX, X[k]);
                     lmaxA = fmax(lmaxA, absol(X[k]));
-                    nxx0[k] = nxx0[k] + qM2[k];
-                    nx[k] = nx[k] + qM2[kGridK + k];
+                    const double Xi = fi + xc;
+                    nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
+                    nx[k] = nx[k] + (Xi - nx[k]) / den;
                     fout[i] = v;
-                    fn[k] = v;
                     Xb[par][i] = X[k];
                 }
-#pragma unroll
-                for (int k = 0; k < kGridK; ++k)
-                    if (k < own) fc[k] = fn[k];
             }
             ix = wave_incl_max(lmaxX, lane);
             ia = wave_incl_max(lmaxA, lane);
@@ -755,13 +724,6 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         // its thread 0 (after the block's __syncthreads) -- a full __threadfence
         // here made every wave write back the L2 again each step
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (j < A.loops) {  // step j+1's neighbours and f[mid], stored by their owners before the barrier
-            if (own > 0) {
-                fL = i0 > 0 ? fout[i0 - 1] : 0.;
-                fR = i0 + own < N ? fout[i0 + own] : 0.;
-            }
-            fmid = fout[mid];
-        }
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
