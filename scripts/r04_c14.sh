@@ -1,8 +1,9 @@
 #!/bin/bash
-# Round-4 calls 14-15: C1 grid kernel A/B/C on one box -- base (before round 4's
-# grid-kernel change), cur (own sites in registers + shared-divisor quotients),
-# new (cur + an acquire-only fence after the grid barrier) -- after the QM1D
-# GPU tests of the new build.
+# Round-4 calls 14-15: C1 grid kernel A/B/C on one box after the QM1D GPU
+# tests of the main build.  Call 14: base (round 3's step), cur (own sites in
+# registers + shared-divisor quotients), new (cur + acquire-only fence after
+# the grid barrier).  Call 15: base, udiv (base + fence + shared-divisor
+# quotients only), new (base + the acquire-only fence).
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-r04_c14}
