@@ -281,7 +281,28 @@ def make_lattice(a, shape, world, rank, local):
     elif world > 1:
         obj = [unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        lat = Phi4Lattice(shape, comm="rccl", nranks=world, rank=rank, comm_id=obj[0], **kw)
+
+        def rccl():
+            q = Phi4Lattice(shape, comm="rccl", nranks=world, rank=rank, comm_id=obj[0], **kw)
+            try:  # one deep-halo block: the first cross-device exchanges, before anything is timed
+                q.step(16)
+                q.sync()
+            except Exception:
+                q.close()
+                raise
+            return q
+
+        def p2p():
+            q = Phi4Lattice(shape, comm="p2p", nranks=world, rank=rank, **kw)
+            connect_p2p(q)
+            return q
+
+        # RCCL with nranks > 1 first runs on the driver's node: should its bring-up
+        # fail on any rank (an error, bounded by the nonblocking init's timeout),
+        # every rank moves to the copy-engine P2P transport together
+        lat, why = open_with_fallback(rccl, p2p, world, dist)
+        a.transport = "rccl" if why is None else "p2p"
+        a.transport_fallback = why
     elif a.comm == "rccl":
         lat = Phi4Lattice(shape, comm="rccl", nranks=1, rank=0, comm_id=unique_id(), **kw)
     elif a.comm == "loopback":
@@ -289,6 +310,28 @@ def make_lattice(a, shape, world, rank, local):
     else:
         lat = Phi4Lattice(shape, **kw)
     return lat, (world > 1 or a.comm != "auto")
+
+
+def open_with_fallback(make_primary, make_fallback, world, dist):
+    """Every rank opens the primary transport; if it failed on ANY rank (agreed
+    by a MIN all-reduce over the host group), every rank closes what it opened
+    and opens the fallback instead.  Returns (lattice, None) or (lattice,
+    reason) -- the reason is this rank's error, or that another rank failed."""
+    import torch
+    lat, err = None, None
+    try:
+        lat = make_primary()
+    except Exception as e:   # the library's error (SQ_E_COMM / SQ_E_HIP), not a hang
+        err = e
+    ok = torch.tensor([0 if lat is None else 1], dtype=torch.int32)
+    if world > 1:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 1:
+        return lat, None
+    if lat is not None:
+        lat.close()
+    why = f"{type(err).__name__}: {err}" if err is not None else "the primary transport failed on another rank"
+    return make_fallback(), why
 
 
 def measure(a, lat, world, slab_path, watch=None):
@@ -622,6 +665,11 @@ def run(a, world, rank, watch):
         watch.finish()
         return
     torch.cuda.set_device(local)
+    a.transport, a.transport_fallback = a.comm, None
+    # RCCL's bring-up and exchanges give up after this (the library's default is
+    # 300 s): short enough that a failed RCCL start still leaves the P2P
+    # fallback and the timed run inside the rank deadline
+    os.environ.setdefault("SQ_COMM_TIMEOUT_S", "90")
     L = a.size
     shape = (L, L, L) if a.strong else (L, L, L * world)
     watch.phase("comm_init", comm=a.comm, shape=list(shape))
@@ -696,9 +744,10 @@ def run(a, world, rank, watch):
                 "ghost_depth": ghost,
                 "block_schedule": schedule,
                 "parallelism": "single GPU, one stream" if not slab_path else
-                               f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else 'rccl'}), halo exchange on "
-                               f"stream B, interior on stream A",
+                               f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else a.transport}), halo "
+                               f"exchange on stream B, interior on stream A",
             },
+            "transport_fallback": a.transport_fallback,
             "roofline": rl,
             "multi_rank_check": check,
             "multi_rank_check_protocol": (f"init 0.1*normal, step counter 0, {verify.CHECK_STEPS} steps; every "
