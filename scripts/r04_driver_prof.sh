@@ -34,7 +34,8 @@ for f in ["$O/trace.log", "$O/bench_driver_1.log", "$O/bench_driver_2.log"]:
             print(f.split("/")[-1], "%.4e" % d["value"], round(d["ms_per_step"] * 1e3, 3), "us/step bound", r["bound"],
                   "frac", r["frac"], "alg", r.get("frac_algorithmic"), "hbm_real", r.get("frac_hbm_real"),
                   "launch_us", r.get("avg_launch_us"), "vs_rocprof", r.get("launch_us_vs_rocprof_avg"),
-                  "busy", r.get("busy_fraction"), "| c3", "%.4e" % d["c3_512"]["value"], d["c3_512"]["roofline"]["frac"],
+                  "busy", r.get("busy_fraction"), "MHz", r.get("clock_MHz_measured"),
+                  "frac_at_clock", r.get("frac_at_measured_clock"), "| c3", "%.4e" % d["c3_512"]["value"], d["c3_512"]["roofline"]["frac"],
                   "| c1", d.get("c1_qm1d", {}).get("value"), d.get("c1_qm1d", {}).get("kernel_ms_per_frame"),
                   (d.get("c1_qm1d", {}).get("cpu_baseline") or {}).get("value"))
 EOF
