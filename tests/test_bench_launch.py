@@ -104,3 +104,20 @@ def test_failing_rank_reports_its_error():
     # fail (the peer's socket closed); both lines name rank 1's error
     assert d["value"] is None and ("terminated" in d["error"] or "rank 0 failed" in d["error"])
     assert d["rank_phases"]["1"]["phase"] == "error" and "injected" in d["rank_phases"]["1"]["error"]
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_default_transport():
+    """The driver's N > 1 path end to end on a one-GPU box: bench.py spawns two
+    ranks on GPU 0 with the default transport.  RCCL refuses two ranks on one
+    device, so the ranks must agree to fall back to P2P together (bench.py
+    open_with_fallback), run, and pass the multi-rank golden-digest check."""
+    d = _run(["--gpus", "2", "--same-device", "--steps", "20", "--warmup", "5", "--no-c3", "--no-c1",
+              "--no-cpu-baseline", "--rank-timeout", "200"], timeout=280)
+    assert d["n_gpus"] == 2 and d["value"] and d["value"] > 0
+    assert d["multi_rank_check"] == "pass"
+    par = d["config"]["parallelism"]
+    if d["transport_fallback"] is not None:
+        assert "(p2p)" in par
+    else:
+        assert "(rccl)" in par
