@@ -14,3 +14,11 @@ python3 scripts/pmc_sq_summary.py $O/fpmc --kernel "6, true, true, false" --json
 python3 scripts/pmc_sq_summary.py $O/fpmc --kernel "1, false, true, false" --json $O/fpmc_raw.json > $O/fpmc_raw.txt 2>&1
 cat $O/fpmc_frame.txt $O/fpmc_raw.txt | grep -i "valu\|wave" | head -12
 find $O/fpmc -name '*counter_collection.csv' -delete
+# frame launches with and without the controller-picked buffers (SQ_FRAME_TRI=0:
+# buffers from the kernel arguments, a snapshot store in each frame's first launch)
+for t in 1 0; do
+  SQ_FRAME_TRI=$t timeout -k 10 300 rocprofv3 --kernel-trace -d $O/ftr$t -o run --output-format csv -- python3 -u scripts/bench_rows_f.py > $O/rows_f_tri$t.log 2>&1 || { tail $O/rows_f_tri$t.log; exit 6; }
+  f=$(find $O/ftr$t -name '*kernel_trace.csv' | head -1)
+  python3 scripts/frame_timeline.py "$f" > $O/frame_timeline_tri$t.txt 2>&1; echo "tri=$t"; cat $O/frame_timeline_tri$t.txt
+  find $O/ftr$t -name '*kernel_trace.csv' -delete
+done
