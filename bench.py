@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--cpu-seconds-c3", type=float, default=8.0, help="target wall time of the 512^3 CPU sample")
     ap.add_argument("--no-c1", action="store_true", help="skip the 32,768-site QM1D chain (configs[0]) sub-record")
     ap.add_argument("--c1-frames", type=int, default=8, help="timed 1000-step frames of the C1 chain")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the frames_256 / slab_1gpu / c1_phi4_32 sub-records of the default run")
     ap.add_argument("--cpu-loops-c1", type=int, default=1000,
                     help="steps of the C1 CPU sample (the reference's serial semantics on one core)")
     ap.add_argument("--rank-timeout", type=float, default=None,
@@ -242,28 +244,51 @@ def cpu_baseline(L, dtau, target_s):
                       f"{cores} threads = this job's CPU share of {os.cpu_count()} host CPUs), {dt:.2f} s"}
 
 
-PROFILE = os.path.join("profiles", "r04", "driver_profile.json")
+PROFILE = os.path.join("profiles", "r05", "driver_profile.json")
 N_SIMD = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_MHZ = 2400.0              # peak engine clock (MI355X_MICROARCH.md)
 VALU_PEAK = N_SIMD * CLOCK_MHZ / 1e3   # G SIMD-cycles/s: every SIMD issuing VALU every cycle
 
 
-def pmc_record(L, kernel):
+def short_kernel(name):
+    """'void sq::(anonymous namespace)::phi4_tb2_kernel<...>(sq::Phi4StepArgs)' -> 'phi4_tb2_kernel<...>'."""
+    name = name.split("(sq::")[0] if "(sq::" in name else name
+    return name.split("::")[-1].strip()
+
+
+def pmc_record(L, launched, build, path=None):
     """The committed rocprofv3 record of the driver's invocation for this lattice
-    (profiles/r04/driver_profile.json, made by scripts/r04_driver_prof.sh +
+    (profiles/r05/driver_profile.json, made by scripts/r05_driver_prof.sh +
     scripts/driver_profile.py from `python3 bench.py --steps 20 --warmup 5`,
     not measured inside this run): PMC HBM bytes and VALU-busy cycles per launch
-    of the fused kernel, and its rocprof dispatch durations."""
-    path = os.path.join(ROOT, PROFILE)
+    of the fused kernel, and its rocprof dispatch durations.
+
+    The record is used only for the binary and launch it describes: its
+    phi4 build id (the hash of the φ⁴ kernels' code object, sq_build_id) must be
+    the loaded library's, its kernel the template instance this run launched
+    most (sq_phi4_launch_info), its grid the same.  Returns (record, path,
+    None), or (None, path, reason) when there is a record for this lattice
+    that does not describe this run (a stale profile), or (None, None, None)
+    when there is none."""
+    rel = path or PROFILE
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, rel)) as fh:
             d = json.load(fh)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     rec = d.get("configs", {}).get(str(L))
-    if not rec or "tb2" not in kernel:
-        return None, None
-    return rec, PROFILE
+    if not rec:
+        return None, None, None
+    why = []
+    if rec.get("build_id_phi4") != build.get("phi4"):
+        why.append(f"build id {rec.get('build_id_phi4')} != loaded {build.get('phi4')}")
+    if short_kernel(rec.get("kernel", "")) != launched.get("kernel"):
+        why.append(f"kernel {short_kernel(rec.get('kernel', ''))} != launched {launched.get('kernel')}")
+    if rec.get("grid") != launched.get("grid"):
+        why.append(f"grid {rec.get('grid')} != launched {launched.get('grid')}")
+    if why:
+        return None, rel, "; ".join(why)
+    return rec, rel, None
 
 
 def make_lattice(a, shape, world, rank, local):
@@ -442,8 +467,12 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
         timing = "wall clock"
     launch_ms = step_ms * spl
     alg = BYTES_PER_SITE * sites_local / (step_ms * 1e-3) / 1e9      # GB/s, 8 B per site update
-    rec, rec_path = pmc_record(L, kname) if (not slab_path and world == 1) else (None, None)
-    r = {"kernel": kname, "timing": timing, "steps_per_launch": round(spl, 3),
+    launched = lat.launch_info()        # the kernel the roofline pass launched most, and its grid
+    from stochquant_amd import _lib
+    build = _lib.build_id()
+    rec, rec_path, stale = pmc_record(L, launched, build) if (not slab_path and world == 1) else (None, None, None)
+    r = {"kernel": launched["kernel"] or kname, "grid_threads": launched["grid"], "kernel_config": kname,
+         "build_id": build, "timing": timing, "steps_per_launch": round(spl, 3),
          "kernel_launches_timed": perf["kernel_launches"],
          "avg_launch_us": round(launch_ms * 1e3, 3), "avg_step_us": round(step_ms * 1e3, 3)}
     valu = None
@@ -457,17 +486,37 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
             "unit": "G VALU-busy SIMD-cycles/s",
             "frac": round(valu / VALU_PEAK, 4),
             "achieved_is": ("VALU-issue cycles of one launch (4 x SQ_ACTIVE_INST_VALU, committed PMC record of "
-                            "this command) / the launch time measured here; peak = 1024 SIMDs x 2.4 GHz"),
+                            "this command, same build id / kernel / grid) / the launch time measured here; "
+                            "peak = 1024 SIMDs x 2.4 GHz"),
         })
-    else:
+    elif fused and stale:
+        # a record exists for this lattice but describes another binary or launch:
+        # no number rather than a confident wrong one
+        r.update({"bound": "valu", "achieved": None, "peak": VALU_PEAK, "unit": "G VALU-busy SIMD-cycles/s",
+                  "frac": None, "stale_profile": True, "stale_reason": stale,
+                  "achieved_is": f"not computed: {rec_path} does not describe this run ({stale})"})
+    elif fused:
+        # no PMC record (other lattice sizes, slab paths, N > 1): the contract's
+        # algorithmic bytes, labelled as such -- a fused launch moves the field
+        # once per two updates, so this ratio is not an HBM measurement
         r.update({
-            "bound": "valu" if fused else "hbm",
+            "bound": "hbm_algorithmic",
             "achieved": round(alg, 1),
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": round(alg / HBM_PEAK_GBPS, 4),
-            "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time"
-                           + ("; no PMC record for this lattice: frac is the algorithmic figure" if fused else ""),
+            "achieved_is": ("algorithmic bytes (8 B per site update, SURVEY.md §8d) / the measured step time; no "
+                            "PMC record for this run, and two-step fused launches move the field once per two "
+                            "updates, so the ratio can exceed 1 and is not a measured HBM fraction"),
+        })
+    else:
+        r.update({
+            "bound": "hbm",
+            "achieved": round(alg, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(alg / HBM_PEAK_GBPS, 4),
+            "achieved_is": "algorithmic bytes (8 B per site update, SURVEY.md §8d) / time (one step per launch)",
         })
     r["frac_algorithmic"] = round(alg / HBM_PEAK_GBPS, 4)
     r["achieved_algorithmic_GBps"] = round(alg, 1)
@@ -491,7 +540,7 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
     if fused and not slab_path and world == 1:
         r.update(busy_fraction(lat, step_ms))
         mhz = r.get("clock_MHz_measured")
-        if mhz and r.get("unit", "").startswith("G VALU"):
+        if mhz and r.get("frac") is not None and r.get("unit", "").startswith("G VALU"):
             # the same VALU cycles against the clock the chip actually ran at
             r["frac_at_measured_clock"] = round(r["frac"] * CLOCK_MHZ / mhz, 4)
     return r, value, fused
@@ -617,6 +666,124 @@ def c1_record(a, local):
     }
 
 
+def frames_record(a, local, nframes=100, loops=20):
+    """tauhost.c:479-560's unit on the north-star lattice: 20-step 256^3 frames
+    (guard, stability rule, rollback, Δτ controller) decided on the device
+    (sq_run_frames), in one batch of `nframes`, against raw 20-step blocks
+    (sq_step) in the same context and run."""
+    import torch
+    from stochquant_amd import Phi4Lattice
+    with Phi4Lattice((256, 256, 256), dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local, loops=loops) as L:
+        L.init_field(0.1)
+        L.run_frames(20)                   # warm-up: code objects, the controller, clocks
+        L.step(200)
+        L.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        st, dts = L.run_frames(nframes)
+        L.sync()
+        tf = time.perf_counter() - t0
+        L.step(400)
+        L.sync()
+        nraw = nframes * loops
+        t0 = time.perf_counter()
+        L.step(nraw)
+        L.sync()
+        tr = time.perf_counter() - t0
+        m = L.moments()
+    us_f = tf * 1e6 / nframes
+    us_raw = tr * 1e6 / nraw * loops
+    return {"config": {"workload": "phi^4 256^3 fp32, frames of 20 Langevin steps through sq_run_frames (the "
+                                   "frame loop of tauhost.c:479-560 on the device: guard flag, stability rule, "
+                                   "rollback, Δτ controller)", "loops": loops, "frames": nframes,
+                       "dtau0": a.dtau, "m2": 1.0, "lambda": 1.0},
+            "us_per_frame": round(us_f, 2), "raw_us_per_20_steps": round(us_raw, 2),
+            "overhead": round(us_f / us_raw - 1.0, 4), "stable_frames": int(st.sum()),
+            "dtau_final": float(dts[-1]) if len(dts) else None,
+            "value": 256 ** 3 * loops * nframes / tf, "unit": "site-updates/s (frames)",
+            "field_check": {"maxabs": m["maxabs"]}}
+
+
+def slab_record(a, local, steps=1000):
+    """SURVEY §8e's slab path on one GPU: the 256^3 lattice as one z-slab whose
+    halo exchange goes through the product's transports to itself (RCCL
+    self-exchange; P2P peer pointers), G = 16 deep halos, fused pairs, the
+    exchange on stream B -- per-step time against the single periodic slab in
+    the same run (the ratio is what the exchange machinery costs before any
+    xGMI)."""
+    import torch
+    from stochquant_amd import Phi4Lattice, unique_id
+    kw = dict(dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local)
+    out = {}
+
+    def timed(L):
+        L.init_field(0.1)
+        L.step(400)
+        L.sync()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        L.step(steps)
+        L.sync()
+        return (time.perf_counter() - t0) * 1e6 / steps
+
+    for name, mk in (("single", lambda: Phi4Lattice((256, 256, 256), **kw)),
+                     ("rccl", lambda: Phi4Lattice((256, 256, 256), comm="rccl", nranks=1, rank=0,
+                                                  comm_id=unique_id(), **kw)),
+                     ("p2p", lambda: Phi4Lattice((256, 256, 256), comm="p2p", nranks=1, rank=0, **kw))):
+        try:
+            with mk() as L:
+                if name == "p2p":
+                    L.p2p_connect([L.p2p_handle()])
+                us = timed(L)
+                sch = L.schedule if name != "single" else None
+            out[name] = {"us_per_step": round(us, 3)}
+            if sch:
+                out[name]["schedule"] = sch
+        except Exception as e:   # the headline record stands without it
+            out[name] = {"error": str(e)[:200]}
+    base = out.get("single", {}).get("us_per_step")
+    for name in ("rccl", "p2p"):
+        if base and "us_per_step" in out[name]:
+            out[name]["ratio_to_single"] = round(out[name]["us_per_step"] / base, 4)
+    out["config"] = {"workload": "phi^4 256^3 fp32 as one z-slab with self-exchange (RCCL / P2P), one GPU",
+                     "steps": steps}
+    return out
+
+
+def c1_phi4_32_record(a, local):
+    """BASELINE configs[0] read literally: a 32^3 φ⁴ lattice, Δτ = 0.01, 1000
+    Langevin steps driven through tauhost.o with taumain.py's 13-argument argv
+    (SQ_MODEL=phi4 SQ_SHAPE=32x32x32: one frame of 1000 steps), its end-file
+    field compared bit for bit with the same frame run through the library."""
+    import tempfile
+    import numpy as np
+    from stochquant_amd import Phi4Lattice, langevin
+    seed, loops, dtau = 0x5EED, 1000, 0.01
+    with tempfile.TemporaryDirectory() as td:
+        end = os.path.join(td, "end_phi4")
+        perf = os.path.join(td, "perf.json")
+        argv = langevin.tauhost_argv(32, 1.0, dtau, 1, 0, 1.0, local, 1, 0, loops, "0", end, 16)
+        env = dict(os.environ, SQ_MODEL="phi4", SQ_SHAPE="32x32x32", SQ_SEED=str(seed), SQ_PERF_JSON=perf)
+        t0 = time.perf_counter()
+        r = langevin.run_tauhost(argv, cwd=td, timeout=120, env=env)
+        wall = time.perf_counter() - t0
+        if r.returncode != 0:
+            return {"error": r.stderr.decode(errors="replace")[-300:]}
+        with open(perf) as fh:
+            pj = json.load(fh)
+        fcli = np.load(end, allow_pickle=False)
+    with Phi4Lattice((32, 32, 32), dtau=dtau, m2=1.0, lam=1.0, seed=seed, device=local, loops=loops) as L:
+        L.init_field(float(np.sqrt(2.0 * dtau)))       # tauhost.o's start field (run_phi4)
+        stable = L.run_frame()
+        flib = L.download()
+    return {"config": {"workload": "BASELINE configs[0] literally: 32^3 scalar phi^4, dt = 0.01, 1000 Langevin "
+                                   "steps, through tauhost.o with taumain.py's argv (SQ_MODEL=phi4)",
+                       "argv": argv[1:], "lattice": [32, 32, 32]},
+            "value": pj.get("site_updates_per_s"), "unit": "site-updates/s (inside the frame)",
+            "frame_seconds": pj.get("frame_seconds"), "process_wall_s": round(wall, 3),
+            "stable": bool(stable), "tauhost_equals_library": bool(np.array_equal(fcli, flib))}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -698,6 +865,19 @@ def run(a, world, rank, watch):
         else:
             digests = [d]
         check = verify.check(digests, shape, world)
+    # parity: the same lattice with the noise off from the
+    # hash field, every rank's slab after CHECK_STEPS steps against the digests
+    # the CPU oracle produced (tests/golden/oracle_slabs.json) -- on every N
+    ocheck = "skipped"
+    watch.phase("oracle_check")
+    if not a.no_check and a.dtau == verify.CHECK_PARAMS["dtau"]:
+        d = verify.run_oracle_protocol(lat, corrupt=(rank == a.corrupt_rank))
+        digests = [None] * world
+        if world > 1:
+            dist.all_gather_object(digests, d)
+        else:
+            digests = [d]
+        ocheck = verify.oracle_check(digests, shape, world)
     ghost = lat.ghost[0] if slab_path else None
     schedule = lat.schedule if slab_path else None
     kname = lat.kernel_name
@@ -750,6 +930,11 @@ def run(a, world, rank, watch):
             "transport_fallback": a.transport_fallback,
             "roofline": rl,
             "multi_rank_check": check,
+            "oracle_check": ocheck,
+            "oracle_check_protocol": (f"C = 0, verify.hash_field initial field, step counter 0, {verify.CHECK_STEPS} "
+                                      f"steps through the same context (same kernels, slabs and exchanges); every "
+                                      f"rank's slab digest vs the CPU oracle's (oracle/orc_phi4.c via "
+                                      f"tests/golden/make_oracle_slabs.py -> tests/golden/oracle_slabs.json)"),
             "multi_rank_check_protocol": (f"init 0.1*normal, step counter 0, {verify.CHECK_STEPS} steps; every "
                                           f"rank's slab digest vs the golden single-GPU run "
                                           f"(stochquant_amd/golden_slabs.json)"),
@@ -791,6 +976,16 @@ def run(a, world, rank, watch):
             out["c1_qm1d"] = c1_record(a, local)
         except Exception as e:  # the headline record stands without it
             out["c1_qm1d"] = {"error": str(e)[:300]}
+    # the frame loop, the one-GPU slab path and the literal configs[0] (VERDICT r4
+    # next #4, #5, #7), measured in the same invocation as the headline
+    if out is not None and world == 1 and not a.strong and a.comm == "auto" and L == 256 and not a.no_extra:
+        for key, fn in (("frames_256", frames_record), ("slab_1gpu", slab_record),
+                        ("c1_phi4_32", c1_phi4_32_record)):
+            watch.phase(key)
+            try:
+                out[key] = fn(a, local)
+            except Exception as e:  # the headline record stands without it
+                out[key] = {"error": str(e)[:300]}
     if world > 1:
         watch.phase("teardown")
         dist.barrier()

@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SQ_ABI_VERSION 4
+#define SQ_ABI_VERSION 5
 
 /* status codes */
 #define SQ_OK 0
@@ -260,6 +260,19 @@ int sq_set_profiling(sq_ctx *ctx, int mode);
 int sq_perf(sq_ctx *ctx, sq_perf_t *out);
 int sq_perf_reset(sq_ctx *ctx);
 int sq_sync(sq_ctx *ctx);
+/* PHI4: the step kernel launched most often since the last sq_perf_reset, as
+ * its template instance (e.g. "phi4_tb2_kernel<true, false, 1, false, true,
+ * false>", the name rocprofv3 prints inside "void sq::(anonymous
+ * namespace)::...(sq::Phi4StepArgs)"), its grid in threads and its launch
+ * count (0 and "" when nothing ran).  Ties a profiler record to the launch. */
+int sq_phi4_launch_info(sq_ctx *ctx, char *name, size_t cap, long long *grid_threads, long long *launches);
+/* Identity of the compiled code: "phi4:<16 hex> lib:<16 hex>", the first a
+ * hash of the φ⁴ kernels' code object, the second of every object linked. */
+const char *sq_build_id(void);
+/* Noise amplitude C (argv[6], sigma = C sqrt(2 Δτ), tau_kernel.cl:112) of an
+ * open context; C = 0 runs the deterministic drift-only update (bench.py's
+ * oracle_check).  Not collective: every rank sets the same C. */
+int sq_set_noise(sq_ctx *ctx, double C);
 /* PHI4, one slab without an exchange, fused launches: run the next two steps
  * (one fused launch, as sq_step(ctx, 2)) with per-block stamps of the
  * constant 100 MHz clock: out[2b], out[2b+1] = start / end of block b

@@ -1,5 +1,5 @@
 """Summarise rocprofv3 runs of the DRIVER's bench invocation into the record
-bench.py's roofline reads (profiles/r04/driver_profile.json).
+bench.py's roofline reads (profiles/r05/driver_profile.json).
 
 Inputs (one rocprofv3 run each, all of `python3 bench.py --steps 20 --warmup 5`,
 MI355X_MICROARCH.md §rocprofv3: counters in passes of their own):
@@ -10,7 +10,9 @@ MI355X_MICROARCH.md §rocprofv3: counters in passes of their own):
 
 For each lattice of the invocation (256^3 = C2, 512^3 = C3) the dominant
 kernel is the two-step fused kernel; its launches are told apart by kernel
-name and grid size.  Per launch:
+name and grid size (the hot instance of each lattice, SIZES below).  The
+record carries the library's build id (sq_build_id: the hash of the φ⁴
+kernels' code object), so bench.py uses it only for that binary.  Per launch:
   * rocprof_avg_us / rocprof_median_us: dispatch durations from the trace
     (every launch of that kernel and grid in the run: settle, warm-up, timed,
     roofline pass);
@@ -22,7 +24,7 @@ name and grid size.  Per launch:
     the physical roofline fraction bench.py reports as `frac` (its live launch
     time in place of rocprof_avg_us).
 
-    python scripts/driver_profile.py --trace D --fetch D --write D --sq D --out profiles/r04/driver_profile.json
+    python scripts/driver_profile.py --trace D --fetch D --write D --sq D --out profiles/r05/driver_profile.json
 """
 import argparse
 import csv
@@ -33,7 +35,9 @@ import statistics
 
 N_SIMD = 1024
 CLOCK_MHZ = 2400.0
-SIZES = {256: 512 * 640, 512: None}   # 256^3: 512 blocks of 10 waves; 512^3 found by elimination
+# the hot instance of each lattice: (template instance, grid in threads or None = its most launched grid)
+SIZES = {256: ("phi4_tb2_kernel<true, false, 1, false, true, false>", 512 * 640),
+         512: ("phi4_tb2p_kernel<true, true, 6, false, true>", None)}
 
 
 def _rows(d, pat):
@@ -78,25 +82,24 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     groups = fused_groups(a.trace)
-    # the two lattices' hot launches: the (kernel, grid) groups with the most launches
-    # (stamp / check-protocol launches are few); 256^3 has the known grid
-    ranked = sorted(groups.items(), key=lambda kv: -len(kv[1]))
-    out = {"command": a.command, "method": __doc__.split("\n\n")[2].strip(), "configs": {}}
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from stochquant_amd import _lib
+    bid = _lib.build_id()
+    out = {"command": a.command, "method": __doc__.split("\n\n")[2].strip(), "build_id": bid, "configs": {}}
     picked = {}
-    for (k, grid), durs in ranked:
-        size = 256 if grid == SIZES[256] else 512
-        if size in picked:
-            continue
-        picked[size] = (k, grid, durs)
-        if len(picked) == 2:
-            break
+    for size, (inst, g0) in SIZES.items():
+        cand = [(k, grid, durs) for (k, grid), durs in groups.items()
+                if "::" + inst + "(" in k and (g0 is None or grid == g0)]
+        if cand:
+            picked[size] = max(cand, key=lambda c: len(c[2]))
     for size, (k, grid, durs) in sorted(picked.items()):
         f, nf = counters(a.fetch, k, grid)
         w, nw = counters(a.write, k, grid)
         s, ns = counters(a.sq, k, grid)
         avg = statistics.fmean(durs)
         med = statistics.median(durs)
-        rec = {"kernel": k, "grid": grid, "launches_in_trace": len(durs),
+        rec = {"kernel": k, "grid": grid, "build_id_phi4": bid.get("phi4"), "launches_in_trace": len(durs),
                "rocprof_avg_us": round(avg, 3), "rocprof_median_us": round(med, 3),
                "rocprof_min_us": round(min(durs), 3), "sites": size ** 3, "steps_per_launch": 2,
                "algorithmic_bytes_per_launch": 8 * size ** 3 * 2, "hbm_min_bytes_per_launch": 8 * size ** 3}

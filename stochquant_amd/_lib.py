@@ -79,7 +79,7 @@ class SqBlockOp(ctypes.Structure):
 
 (SQ_OP_EXCHANGE, SQ_OP_STEP, SQ_OP_PAIR, SQ_OP_WAIT_EXCHANGE, SQ_OP_EDGES_DONE, SQ_OP_WAIT_STAGED, SQ_OP_SIGNAL,
  SQ_OP_WAIT) = range(8)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 _P = ctypes.c_void_p
@@ -137,6 +137,10 @@ SIGNATURES = {
     "sq_perf": (ctypes.c_int, [_P, ctypes.POINTER(SqPerf)]),
     "sq_perf_reset": (ctypes.c_int, [_P]),
     "sq_sync": (ctypes.c_int, [_P]),
+    "sq_phi4_launch_info": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_longlong),
+                                           ctypes.POINTER(ctypes.c_longlong)]),
+    "sq_build_id": (ctypes.c_char_p, []),
+    "sq_set_noise": (ctypes.c_int, [_P, ctypes.c_double]),
     "sq_phi4_block_stamps": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, _I]),
     "sq_phi4_block_clocks": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int, _I]),
     "sq_comm_unique_id": (ctypes.c_int, [ctypes.POINTER(ctypes.c_ubyte)]),
@@ -196,6 +200,12 @@ def default_params():
     p = SqParams()
     load().sq_params_init(ctypes.byref(p))
     return p
+
+
+def build_id():
+    """{"phi4": <hash of the φ⁴ kernels' code object>, "lib": <hash of every object>} of the loaded library."""
+    s = load().sq_build_id().decode()
+    return dict(kv.split(":", 1) for kv in s.split() if ":" in kv) or {"raw": s}
 
 
 def device_count():

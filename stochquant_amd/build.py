@@ -44,6 +44,18 @@ def _digest(paths, extra):
     return h.hexdigest()
 
 
+def build_id(objs):
+    """"phi4:<h> lib:<h>": sha256 (16 hex) of the φ⁴ kernels' object, and of every object in link order."""
+    def h(paths):
+        d = hashlib.sha256()
+        for p in paths:
+            with open(p, "rb") as fh:
+                d.update(fh.read())
+        return d.hexdigest()[:16]
+    phi4 = [o for o in objs if os.path.basename(o) == "sq_phi4.hip.o"]
+    return f"phi4:{h(phi4)} lib:{h(objs)}"
+
+
 def _run(cmd):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
@@ -74,8 +86,19 @@ def build(force=False, verbose=False):
             if verbose:
                 print(" ".join(cmd))
     objs = [os.path.join(OBJ, s + ".o") for s in DEVICE_SOURCES + HOST_SOURCES]
+    bid = build_id(objs)
+    bid_obj = os.path.join(OBJ, "sq_build_id.cpp.o")
+    bid_stamp = bid_obj + ".sha"
+    if jobs or force or not os.path.exists(bid_obj) or not os.path.exists(bid_stamp) or \
+            open(bid_stamp).read() != bid:
+        # the identity of the objects just built, compiled into the library (sq_build_id)
+        _run([HIPCC] + COMMON + ["-x", "c++", f'-DSQ_BUILD_ID="{bid}"', "-c",
+                                 os.path.join(CSRC, "sq_build_id.cpp"), "-o", bid_obj])
+        with open(bid_stamp, "w") as fh:
+            fh.write(bid)
+        jobs.append(None)
     if jobs or force or not os.path.exists(LIB):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [bid_obj]
              + [f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"])
     th_src = os.path.join(CSRC, "tauhost.cpp")
     if jobs or force or not os.path.exists(TAUHOST) or \

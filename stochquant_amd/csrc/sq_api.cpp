@@ -18,6 +18,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <string>
 #include <thread>
 #include <vector>
@@ -276,6 +277,10 @@ struct sq_ctx {
     size_t ev_used = 0;
     long long region_steps = 0;
     sq_perf_t perf{};
+    // step-kernel launches since the last sq_perf_reset by kernel id (template
+    // instance + grid, sq::phi4_kernel_id_name): sq_phi4_launch_info names the
+    // dominant one, which bench.py matches against its committed PMC record
+    std::map<uint64_t, long long> kstat;
 };
 
 namespace {
@@ -487,8 +492,10 @@ int phi4_launch_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int 
         int rc = ev_take(c, &e);
         if (rc) return rc;
     }
-    SQ_HIP(sq::phi4_step_launch(a, c->geom, st, e ? e->a : nullptr, e ? e->b : nullptr));
+    uint64_t kid = 0;
+    SQ_HIP(sq::phi4_step_launch(a, c->geom, st, e ? e->a : nullptr, e ? e->b : nullptr, &kid));
     c->perf.kernel_launches += 1;
+    c->kstat[kid] += 1;
     return SQ_OK;
 }
 
@@ -571,19 +578,22 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
         if (rc) return rc;
         c->ev_extra_steps += 1;
     }
-    if (a.stamps != nullptr) {
-        if (a.nunits > c->stamps_cap) return fail(SQ_E_STATE, "block stamps: more blocks than stamp slots");
-        c->stamps_blocks = a.nunits;
+    if (a.stamps != nullptr) {  // every block of the grid stamps (a gated launch adds its rim chunks)
+        const int grid_n = a.nunits + (a.gate != nullptr ? a.nxseg * a.nyg * 2 * a.ntz : 0);
+        if (grid_n > c->stamps_cap) return fail(SQ_E_STATE, "block stamps: more blocks than stamp slots");
+        c->stamps_blocks = grid_n;
     }
     hipEvent_t stop = c->stop_next;
     c->stop_next = nullptr;
+    uint64_t kid = 0;
     if (e == nullptr && stop != nullptr) {
-        SQ_HIP(sq::phi4_tb2_launch(a, st, nullptr, stop));
+        SQ_HIP(sq::phi4_tb2_launch(a, st, nullptr, stop, &kid));
         c->stop_used = true;
     } else {
-        SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr));
+        SQ_HIP(sq::phi4_tb2_launch(a, st, e ? e->a : nullptr, e ? e->b : nullptr, &kid));
     }
     c->perf.kernel_launches += 1;
+    c->kstat[kid] += 1;
     c->perf.fused_steps += 2;
     return SQ_OK;
 }
@@ -1575,6 +1585,9 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
     SQ_HIP(hipMemcpyAsync(&st, c->qst, sizeof st, hipMemcpyDeviceToHost, c->qstream));
     SQ_HIP(hipStreamSynchronize(c->qstream));
+    if (st.sync_error)  // qm1d_frame_grid: a grid barrier gave up; nothing of the frame is adopted
+        return fail(SQ_E_HIP, "QM1D grid barrier timeout: a block of qm1d_frame_grid never arrived "
+                              "(the frame is void, the state is the frame start)");
     c->step += (unsigned long long)c->p.loops;
     c->lrgEl = st.lrgEl;
     c->lrgVl = st.lrgVl;
@@ -2325,7 +2338,11 @@ int sq_sync(sq_ctx *c) {
     if (c->gate_err) {  // a gated rim chunk gave up waiting for its exchange (tb_gate_wait)
         int e = 0;
         SQ_HIP(hipMemcpy(&e, c->gate_err, sizeof e, hipMemcpyDeviceToHost));
-        if (e) return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange");
+        if (e) {  // reported once: cleared, so later calls see only new timeouts
+            SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
+            return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange (their "
+                                   "chunks were not stored)");
+        }
     }
     return SQ_OK;
 }
@@ -2644,6 +2661,32 @@ int sq_perf_reset(sq_ctx *c) {
     int rc = flush_events(c);
     if (rc) return rc;
     c->perf = sq_perf_t{};
+    c->kstat.clear();
+    return SQ_OK;
+}
+
+int sq_phi4_launch_info(sq_ctx *c, char *name, size_t cap, long long *grid_threads, long long *launches) {
+    if (!c || !name || cap == 0) return fail(SQ_E_ARG, "bad argument");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    name[0] = 0;
+    uint64_t best = 0;
+    long long n = 0;
+    for (const auto &kv : c->kstat)  // most launches; ties: the larger grid (the map is ordered by id)
+        if (kv.second > n || (kv.second == n && sq::phi4_kernel_id_grid(kv.first) > sq::phi4_kernel_id_grid(best))) {
+            best = kv.first;
+            n = kv.second;
+        }
+    if (n > 0) sq::phi4_kernel_id_name(best, name, cap);
+    if (grid_threads) *grid_threads = n > 0 ? (long long)sq::phi4_kernel_id_grid(best) : 0;
+    if (launches) *launches = n;
+    return SQ_OK;
+}
+
+int sq_set_noise(sq_ctx *c, double C) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    // the PHI4 guard fast path bounds |sigma xi| by 16 sqrt(2 dtau) |C| (create_phi4), dtau <= 1e20
+    if (!std::isfinite(C) || std::fabs(C) > 1e12) return fail(SQ_E_ARG, "C must be finite, |C| <= 1e12");
+    c->p.C = C;
     return SQ_OK;
 }
 

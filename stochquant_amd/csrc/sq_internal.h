@@ -186,7 +186,14 @@ struct Phi4Geom {
 // Bit-identical to two step launches.
 bool phi4_tb2_supported(int Lx, int Ly);
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t start = nullptr,
-                           hipEvent_t stop = nullptr);
+                           hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
+
+// Kernel identity of a launch (kid out-parameters of the launchers): the
+// template instance the launcher picked, packed with the grid in threads (high
+// 32 bits), so a caller can name the dominant kernel exactly as rocprofv3 does
+// (sq_phi4_launch_info; bench.py ties its committed PMC record to it).
+void phi4_kernel_id_name(uint64_t kid, char *name, size_t cap);
+inline unsigned phi4_kernel_id_grid(uint64_t kid) { return (unsigned)(kid >> 32); }
 
 // Picks the register tile for (Lx, Ly); returns false if unsupported.
 bool phi4_geometry(int Lx, int Ly, Phi4Geom *g);
@@ -195,7 +202,7 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g);
 // start/stop non-null: timed through hipExtLaunchKernel (timestamps of the
 // dispatch itself, no extra marker packets on the stream).
 hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s,
-                            hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+                            hipEvent_t start = nullptr, hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
 // slab = local plane 0 (past the ghost zone)
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
@@ -224,7 +231,7 @@ struct Qm1dState {    // device-resident frame scalars
     int lrgEl;        // carried leader index (tauhost.c:65)
     int stable;       // 1 stable, 0 unstable
     int steps_done;
-    int pad;
+    int sync_error;   // qm1d_frame_grid: a grid barrier gave up waiting (kGridSpinMax polls); the frame is void
 };
 
 struct Qm1dArgs {
@@ -246,6 +253,8 @@ struct Qm1dArgs {
     uint32_t k0, k1;
     unsigned long long tick;    // Philox step index of the frame's first step
     int gbar;                   // qm1d_frame_grid: 1 = its own counter barrier (else cooperative groups)
+    unsigned int bar_polls;     // ... the barrier's poll budget (0: kGridSpinMax)
+    int bar_skip;               // ... (tests, SQ_QM1D_BAR_SKIP) this block never arrives at barrier 1; -1 none
 };
 
 int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant: N > kQm1dRegMaxN)

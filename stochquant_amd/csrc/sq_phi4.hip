@@ -20,6 +20,7 @@
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "sq_dpp.h"
@@ -917,19 +918,27 @@ __device__ __forceinline__ TbBlock tb_block(const Phi4StepArgs &A, int b, int nb
 // polls the block gives up and flags gate_err (the host reports it), so a lost
 // exchange ends as an error, not a hung grid.
 constexpr unsigned int kGateSpinMax = 1u << 24;  // ~1 s of s_sleep 2
-__device__ __forceinline__ void tb_gate_wait(const Phi4StepArgs &A) {
+// Returns false when the wait gave up: the block then stores nothing (its
+// ghost planes are stale), so a timed-out exchange leaves the chunk's previous
+// contents, never values computed from an unfinished exchange.
+__device__ __forceinline__ bool tb_gate_wait(const Phi4StepArgs &A) {
+    __shared__ int s_gate_ok;
     if (threadIdx.x == 0) {
         unsigned int n = 0;
+        int ok = 1;
         while (__hip_atomic_load(A.gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < A.gate_seq) {
             __builtin_amdgcn_s_sleep(2);
             if (++n >= kGateSpinMax) {
                 if (A.gate_err) __hip_atomic_fetch_or(A.gate_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
                 break;
             }
         }
+        s_gate_ok = ok;
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return s_gate_ok != 0;
 }
 
 constexpr int kTbRows = 8;
@@ -1203,7 +1212,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2_kernel(const Phi4StepArg
     __shared__ float4 lds[3][kTbWaves][64];
     __shared__ float tx[WIDE ? 3 : 1][kTbWaves][2];
 
-    if (tbk.gated) tb_gate_wait(A);  // a rim chunk: its input's ghost planes come with the exchange
+    if (tbk.gated && !tb_gate_wait(A)) return;  // a rim chunk: its input's ghost planes come with the exchange
     TbIn I0, I1, I2;
     {
         const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
@@ -1484,7 +1493,7 @@ __attribute__((amdgpu_waves_per_eu(WPE))) void phi4_tb2p_kernel(const Phi4StepAr
     __shared__ float4 t_lds[2][kTbWaves][64];
     __shared__ float tx[WIDE ? 2 : 1][kTbWaves][2];
 
-    if (tbk.gated) tb_gate_wait(A);  // a rim chunk: its input's ghost planes come with the exchange
+    if (tbk.gated && !tb_gate_wait(A)) return;  // a rim chunk: its input's ghost planes come with the exchange
     // prologue: planes z0-2, z0-1, z0 (own rows), the rows beyond of z0-1 and
     // z0, edge sites / x-halo neighbours of plane z0-1; plane z0-1 published
     const __amdgpu_buffer_rsrc_t p0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
@@ -1900,11 +1909,41 @@ static hipError_t launch_r(const Phi4StepArgs &a, const Phi4Geom &g, dim3 grid, 
     }
 }
 
+// Kernel ids (phi4_kernel_id_name): bits 0-1 family (0 phi4_step_kernel, 1
+// phi4_tb2_kernel, 2 phi4_tb2p_kernel), 2 NZ, 3 WIDE / MS, 4-7 WPE, 8 FR, 9 WH,
+// 10 P2, 11-18 QX, 19-22 R, 23-24 V, 25-28 PF; bits 32-63 the grid in threads.
+static uint64_t kid_pack(int fam, bool nz, bool wide, int e, bool fr, bool wh, bool p2, int qx, int r, int v,
+                         int pf, unsigned threads) {
+    return (uint64_t)fam | (uint64_t)nz << 2 | (uint64_t)wide << 3 | (uint64_t)(e & 15) << 4 | (uint64_t)fr << 8 |
+           (uint64_t)wh << 9 | (uint64_t)p2 << 10 | (uint64_t)(qx & 255) << 11 | (uint64_t)(r & 15) << 19 |
+           (uint64_t)(v & 3) << 23 | (uint64_t)(pf & 15) << 25 | (uint64_t)threads << 32;
+}
+
+void phi4_kernel_id_name(uint64_t k, char *name, size_t cap) {
+    const int fam = (int)(k & 3);
+    auto b = [&](int bit) { return ((k >> bit) & 1) ? "true" : "false"; };
+    const int e = (int)((k >> 4) & 15), qx = (int)((k >> 11) & 255), r = (int)((k >> 19) & 15),
+              v = (int)((k >> 23) & 3), pf = (int)((k >> 25) & 15);
+    if (fam == 0)
+        snprintf(name, cap, "phi4_step_kernel<%d, %d, %d, %s, %s, %d, %s>", qx, r, v, b(3), b(2), pf, b(8));
+    else if (fam == 1)
+        snprintf(name, cap, "phi4_tb2_kernel<%s, %s, %d, %s, %s, %s>", b(2), b(3), e, b(8), b(9), b(10));
+    else
+        snprintf(name, cap, "phi4_tb2p_kernel<%s, %s, %d, %s, %s>", b(2), b(3), e, b(8), b(9));
+}
+
 hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s, hipEvent_t e0,
-                            hipEvent_t e1) {
+                            hipEvent_t e1, uint64_t *kid) {
     if (a.nunits <= 0) return hipSuccess;
     const dim3 grid((unsigned)((a.nunits + 3) / 4));
     const bool ms = a.nxseg > 1;
+    if (kid != nullptr) {  // the instance launch_r / launch_v / launch_pf pick below
+        const bool q64 = g.qx == 64;
+        const int r = g.r == 4 ? 4 : g.r == 2 ? 2 : 1;
+        const int pf = q64 && (g.pf == 3 || g.pf == 4 || g.pf == 7) ? g.pf : 1;
+        *kid = kid_pack(0, a.sig != 0.0f, q64 && ms, 0, a.flag != nullptr, false, false, g.qx, r,
+                        q64 && g.v == 2 ? 2 : 1, pf, grid.x * 256u);
+    }
     switch (g.qx) {
     case 64:
         if (g.v == 2) return ms ? launch_r<64, 2, true>(a, g, grid, s, e0, e1) : launch_r<64, 2, false>(a, g, grid, s, e0, e1);
@@ -1925,7 +1964,7 @@ static bool tb2_sync_p2p() {
     return e != nullptr && strcmp(e, "p2p") == 0;
 }
 
-hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, hipEvent_t e1, uint64_t *kid) {
     if (!phi4_tb2_supported(a.Lx, a.Ly) || a.nunits <= 0 || a.nxseg != a.Lx / 256 || a.nyg != a.Ly / kTbRows ||
         a.nzr < 1 || a.nzc % a.nzr != 0 || a.nunits != a.nxseg * a.nyg * a.nzc || a.zlen < 1 ||
         (long long)a.zc * a.nzr < a.zlen)
@@ -1986,6 +2025,11 @@ hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t e0, 
 #undef SQ_TB2
 #undef SQ_TB2F
 #undef SQ_TB2K
+    if (kid != nullptr) {  // the same choice as above, as a kernel id
+        const bool p2 = !wide && !pipe && tb2_sync_p2p();
+        const int e = wide ? (wpe == 6 ? 6 : 1) : (fr ? 6 : 1);
+        *kid = kid_pack(pipe && !p2 ? 2 : 1, nz, wide, e, fr, wh, p2, 0, 0, 0, 0, grid.x * block.x);
+    }
     Phi4StepArgs q = a;
     // wave priority by march progress: 256^3 16.3-16.7 vs 17.0 us/step, 512^3
     // 135-137 vs 140-141 (profiles/r03/prio); SQ_TB2_PRIO=0 turns it off

@@ -603,15 +603,34 @@ constexpr int kGridT = 256;
 // each block releases its block's writes, counts the block in and spins until
 // every block of barrier `n` (1-based) has; the counter was zeroed ahead of the
 // launch.  A vector atomic and a relaxed load, no scalar-memory writes.
-__device__ __forceinline__ void grid_barrier(unsigned int *ctr, unsigned int n) {
+// Bounded: the plain launch leaves co-residency to the host's occupancy check
+// (qm1d_frame_launch), so a block that is never scheduled -- or never arrives
+// -- must not hang the process.  After `polls` polls (or once another block has
+// given up, err != 0) the block raises *err and the barrier returns false: the
+// caller's block leaves the kernel, every other block then gives up in turn,
+// and the host reports the frame as failed (Qm1dState::sync_error).
+constexpr unsigned int kGridSpinMax = 1u << 22;  // ~2-4 s of polls; a barrier normally waits a few us
+__device__ __forceinline__ bool grid_barrier(unsigned int *ctr, unsigned int n, int *err, unsigned int polls,
+                                             bool skip) {
+    __shared__ int s_ok;
     __syncthreads();
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (!skip) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned int target = n * gridDim.x;
-        while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target)
+        int ok = 1;
+        for (unsigned int k = 0; __hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target; ++k) {
+            if (k >= polls ||
+                ((k & 1023u) == 1023u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
+        }
+        s_ok = ok;
     }
     __syncthreads();
+    return s_ok != 0;
 }
 
 template <int kGridK>
@@ -716,10 +735,13 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                 bm[(2 * par + 1) * G + b] = ba;
             }
         }
-        if (A.gbar)
-            grid_barrier(bar, (unsigned int)(j + 1));
-        else
+        if (A.gbar) {
+            if (!grid_barrier(bar, (unsigned int)(j + 1), &A.st->sync_error, A.bar_polls ? A.bar_polls : kGridSpinMax,
+                              j == 0 && b == A.bar_skip))
+                return;  // a barrier gave up: the frame is void (the host reports it)
+        } else {
             grid.sync();
+        }
         // acquire only: every block's writes before the barrier were released by
         // its thread 0 (after the block's __syncthreads) -- a full __threadfence
         // here made every wave write back the L2 again each step
@@ -879,6 +901,10 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         // cooperative groups' grid.sync (profiles/r03/qm1d_grid/); SQ_QM1D_BAR=0
         const char *gb = getenv("SQ_QM1D_BAR");
         q.gbar = gb ? atoi(gb) : 1;
+        // tests: a block that never arrives (SQ_QM1D_BAR_SKIP=b) and a shorter poll budget
+        const char *bs = getenv("SQ_QM1D_BAR_SKIP"), *bp = getenv("SQ_QM1D_BAR_POLLS");
+        q.bar_skip = bs ? atoi(bs) : -1;
+        q.bar_polls = bp ? (unsigned int)strtoul(bp, nullptr, 10) : 0u;
         if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (after the tagged words)
             hipError_t e = hipMemsetAsync(reinterpret_cast<unsigned int *>(q.ds + q.N) + 4, 0, sizeof(unsigned int), s);
             if (e != hipSuccess) return e;

@@ -110,6 +110,11 @@ class _Ctx:
     def sync(self):
         _lib.call("sq_sync", self._h)
 
+    def set_noise(self, C):
+        """Noise amplitude C of the open context (C = 0: drift only, deterministic)."""
+        _lib.call("sq_set_noise", self._h, float(C))
+        self.params.C = float(C)
+
 
 class Qm1dChain(_Ctx):
     """The reference's 1-D chain: N sites (Δt spacing), potID 0 or 3, noise C,
@@ -274,6 +279,14 @@ class Phi4Lattice(_Ctx):
         buf = ctypes.create_string_buffer(160)
         _lib.call("sq_phi4_kernel", self._h, buf, len(buf))
         return buf.value.decode()
+
+    def launch_info(self):
+        """The step kernel launched most often since perf_reset(): {"kernel": template
+        instance as rocprofv3 names it, "grid": threads, "launches": n}."""
+        buf = ctypes.create_string_buffer(160)
+        g, n = ctypes.c_longlong(), ctypes.c_longlong()
+        _lib.call("sq_phi4_launch_info", self._h, buf, len(buf), ctypes.byref(g), ctypes.byref(n))
+        return {"kernel": buf.value.decode(), "grid": g.value, "launches": n.value}
 
     @property
     def ghost(self):

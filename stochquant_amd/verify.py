@@ -52,6 +52,73 @@ def check(digests, shape, nranks, golden=None):
     return "pass" if all(d == e for d, e in zip(digests, g["slabs"])) else "fail"
 
 
+ORACLE_GOLDEN = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                             "oracle_slabs.json")
+HASH_FIELD_KEY = 0x5EED5EED
+HASH_FIELD_AMP = 0.25
+
+
+def hash_field(shape, z0, nz, chunk=16):
+    """The oracle check's initial field: planes [z0, z0 + nz) of a global
+    (Lx, Ly, Lz) lattice, numpy order (z, y, x), float32.  Site i (global
+    index (z Ly + y) Lx + x) gets splitmix64(i ^ key)'s top 24 bits as a
+    uniform value in [-AMP, AMP): integer arithmetic and one exact scaling,
+    identical on every host, so each rank builds its own slab and the oracle
+    the whole lattice without a device RNG in between."""
+    Lx, Ly, _ = shape
+    out = np.empty((nz, Ly, Lx), dtype=np.float32)
+    plane = Lx * Ly
+    for c0 in range(0, nz, chunk):
+        c1 = min(nz, c0 + chunk)
+        i = np.arange((z0 + c0) * plane, (z0 + c1) * plane, dtype=np.uint64) ^ np.uint64(HASH_FIELD_KEY)
+        # splitmix64 finaliser (wrapping uint64 arithmetic)
+        i = i + np.uint64(0x9E3779B97F4A7C15)
+        i = (i ^ (i >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        i = (i ^ (i >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        i = i ^ (i >> np.uint64(31))
+        u = (i >> np.uint64(40)).astype(np.float64)          # [0, 2^24)
+        out[c0:c1] = ((u - 8388608.0) * (HASH_FIELD_AMP / 8388608.0)).reshape(c1 - c0, Ly, Lx)
+    return out
+
+
+def load_oracle_golden(path=ORACLE_GOLDEN):
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
+def run_oracle_protocol(lat, corrupt=False):
+    """The noise-off parity protocol (collective in multi-rank contexts): C = 0,
+    this rank's slab of hash_field uploaded, the step counter at 0,
+    CHECK_STEPS steps; returns the slab digest.  With the noise off the step is
+    deterministic fp32 arithmetic, so the digest must equal the oracle's
+    (oracle/orc_phi4.c, tests/golden/make_oracle_slabs.py) bit for bit."""
+    C0 = float(lat.params.C)
+    lat.set_noise(0.0)
+    try:
+        lat.upload(hash_field(lat.shape, lat.z0, lat.nz_local))
+        lat.step_counter = 0
+        lat.step(CHECK_STEPS)
+        f = lat.download()
+        if corrupt:
+            f.flat[f.size // 2] += np.float32(1.0)
+        return slab_digest(f)
+    finally:
+        lat.set_noise(C0)
+
+
+def oracle_check(digests, shape, nranks, golden=None):
+    """'pass' / 'fail' / 'no golden' of the noise-off digests against the oracle's."""
+    g = (load_oracle_golden() if golden is None else golden).get(golden_key(shape, nranks))
+    if g is None:
+        return "no golden"
+    if len(digests) != nranks or len(g["slabs"]) != nranks:
+        return "fail"
+    return "pass" if all(d == e for d, e in zip(digests, g["slabs"])) else "fail"
+
+
 def run_protocol(lat, corrupt=False):
     """Run the check protocol on an open Phi4Lattice (collective in multi-rank
     contexts) and return this rank's slab digest.  corrupt: flip one value of

@@ -906,8 +906,9 @@ RUN_FRAMES_CASES = [((256, 16, 16), 6, {}), ((256, 8, 12), 5, {}), ((64, 16, 8),
                     ((512, 8, 6), 4, {}), ((256, 8, 12), 6, {"comm": "loopback", "nslabs": 3})]
 
 
+@pytest.mark.parametrize("tri", ["1", "0"])
 @pytest.mark.parametrize("shape,loops,kw", RUN_FRAMES_CASES)
-def test_run_frames_match_host_frames(gpu, oracle_mod, monkeypatch, shape, loops, kw):
+def test_run_frames_match_host_frames(gpu, oracle_mod, monkeypatch, shape, loops, kw, tri):
     """sq_run_frames (verdict, rollback and Δτ controller on the device between
     frames) and sq_run_frame per frame equal the host-decided
     frames (SQ_FRAME_HOST=1: record read-back, stab_rule and adapt on the host)
@@ -915,8 +916,11 @@ def test_run_frames_match_host_frames(gpu, oracle_mod, monkeypatch, shape, loops
     T / V and the last frame's records.  Δτ starts above the Euler limit, so
     the run mixes rolled-back frames (Δτ x 0.95) with stable ones (Δτ / 0.95
     after 11); fused (even and odd frame lengths), per-step, 512-wide and
-    multi-slab (host path) contexts."""
+    multi-slab (host path) contexts; three buffers (tri = 1, the default) and
+    the snapshot fold path (SQ_FRAME_TRI=0: an unstable verdict rolls back by
+    reading the padded snapshot and skips the snapshot store)."""
     nfr = 40
+    monkeypatch.setenv("SQ_FRAME_TRI", tri)
 
     def run(mode):
         monkeypatch.setenv("SQ_FRAME_HOST", "1" if mode == "host" else "0")
@@ -995,3 +999,107 @@ def test_block_stamps_are_two_steps(gpu, oracle_mod):
         assert 100.0 <= mhz <= 3000.0, mhz
         assert L.step_counter == R.step_counter == 3
         assert np.array_equal(L.download(), R.download())
+
+
+HOT_256 = "phi4_tb2_kernel<true, false, 1, false, true, false>"
+
+
+def test_c2_hot_instance_vs_oracle(gpu, oracle_mod, bm_tables):
+    """The exact instance the bench times at 256^3 (VERDICT r4 next #1c), not
+    a neighbour of it: a default context, the bench's init_field(0.1) (seed
+    0x5EED, Δτ = 0.01, m² = λ = 1), 6 steps = 3 fused launches of
+    phi4_tb2_kernel<true, false, 1, false, true, false> (the guard fast path on:
+    the field came from init_field), compared with the oracle from the same
+    initial field -- bitwise with the device's Box-Muller factors, within
+    6 x the per-step bound (STEP_ATOL + STEP_RTOL |phi'|) of the mathematical
+    normals.  The initial field itself is the oracle's phi4_init bit for bit
+    in device-transcendental mode."""
+    shape = (256, 256, 256)
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED) as L:
+        L.init_field(0.1)
+        phi0 = L.download()
+        L.perf_reset()
+        L.step(6)
+        got = L.download()
+        info = L.launch_info()
+        perf = L.perf()
+    assert info["kernel"] == HOT_256 and info["launches"] == 3, info
+    assert info["grid"] == 512 * 640, info          # one round of 512 ten-wave blocks
+    assert perf["fused_steps"] == 6 and perf["kernel_launches"] == 3
+    p = oracle_mod.phi4_params(shape, 0.01, 1.0, 1.0, 0x5EED)
+    with oracle_mod.device_transcendentals(bm_tables):
+        assert np.array_equal(phi0, oracle_mod.phi4_init(p, 0.1))
+        ref_dev = _oracle_run(oracle_mod, shape, phi0, 6, C=1.0, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED)
+    assert np.array_equal(got, ref_dev), f"max diff {np.max(np.abs(got - ref_dev))}"
+    del ref_dev
+    ref = _oracle_run(oracle_mod, shape, phi0, 6, C=1.0, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED)
+    err = np.abs(got.astype(np.float64) - ref)
+    assert np.all(err <= 6 * (STEP_ATOL + STEP_RTOL * np.abs(ref))), f"max err {err.max()}"
+
+
+@pytest.mark.parametrize("shape,kw", [((256, 16, 40), {}), ((256, 16, 40), {"comm": "loopback", "nslabs": 3}),
+                                      ((256, 16, 48), {"comm": "rccl"}), ((512, 8, 33), {}),
+                                      ((64, 16, 24), {})])
+def test_oracle_protocol_matches_oracle(gpu, oracle_mod, shape, kw):
+    """bench.py's oracle_check protocol (verify.run_oracle_protocol: C = 0 set
+    on the open context, the hash field uploaded, CHECK_STEPS steps) on small
+    lattices, single slab / loopback slabs / RCCL self-exchange: the field is
+    the oracle's bit for bit, and the context's noise comes back on."""
+    from stochquant_amd import unique_id, verify
+    if kw.get("comm") == "rccl":
+        kw = dict(kw, nranks=1, rank=0, comm_id=unique_id())
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, **kw) as L:
+        d = verify.run_oracle_protocol(L)
+        got = L.download()
+        assert L.params.C == 1.0
+        L.init_field(0.1)
+        L.step(2)
+        noisy = L.download()
+    p = oracle_mod.phi4_params(shape, 0.01, 1.0, 1.0, 0x5EED, C=0.0)
+    ref = verify.hash_field(shape, 0, shape[2])
+    for s in range(verify.CHECK_STEPS):
+        ref = oracle_mod.phi4_step(p, ref, s)
+    assert np.array_equal(got, ref), f"max diff {np.max(np.abs(got - ref))}"
+    assert d == verify.slab_digest(ref)
+    if "comm_id" in kw:
+        kw["comm_id"] = unique_id()
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED, **kw) as L:   # the noise is back on
+        L.init_field(0.1)
+        L.step_counter = verify.CHECK_STEPS
+        L.step(2)
+        assert np.array_equal(L.download(), noisy)
+
+
+def test_oracle_check_full_size_256(gpu):
+    """The bench's oracle_check at N = 1 (256^3, the committed oracle digest of
+    tests/golden/oracle_slabs.json): pass; a flipped value fails."""
+    from stochquant_amd import verify
+    shape = (256, 256, 256)
+    with _lat(shape, dtau=0.01, m2=1.0, lam=1.0, seed=0x5EED) as L:
+        d = verify.run_oracle_protocol(L)
+        bad = verify.run_oracle_protocol(L, corrupt=True)
+    assert verify.oracle_check([d], shape, 1) == "pass"
+    assert verify.oracle_check([bad], shape, 1) == "fail"
+
+
+def test_launch_info_names_each_instance(gpu, monkeypatch):
+    """sq_phi4_launch_info: the dominant step kernel's template instance and
+    grid, per the launcher's own choice (the per-step kernel, the 512-wide
+    pipelined fused kernel, the noise-off instance)."""
+    with _lat((256, 16, 16), dtau=0.01) as L:
+        L.step(4)
+        assert L.launch_info()["kernel"].startswith("phi4_tb2_kernel<true, false, 1, false, true, false>")
+        L.set_noise(0.0)
+        L.perf_reset()
+        L.step(4)
+        assert L.launch_info()["kernel"] == "phi4_tb2_kernel<false, false, 1, false, true, false>"
+        L.perf_reset()
+        assert L.launch_info() == {"kernel": "", "grid": 0, "launches": 0}
+    with _lat((512, 8, 16), dtau=0.01) as L:
+        L.step(2)
+        assert L.launch_info()["kernel"] == "phi4_tb2p_kernel<true, true, 6, false, true>"
+    monkeypatch.setenv("SQ_FUSE2", "0")
+    with _lat((32, 32, 32), dtau=0.01) as L:
+        L.step(3)
+        info = L.launch_info()
+        assert info["kernel"].startswith("phi4_step_kernel<32, ") and info["launches"] == 3, info

@@ -225,3 +225,33 @@ def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h):
     for k in ("f", "x", "xx0"):
         assert np.array_equal(d1[k], d0[k]), k
     assert d1["omega"] == d0["omega"] and c1 == c0
+
+
+def test_grid_barrier_timeout_returns_error(gpu, monkeypatch):
+    """The grid kernel's counter barrier is bounded: with a
+    debug switch one block never arrives at the first barrier
+    (SQ_QM1D_BAR_SKIP), every block gives up after its poll budget, and the
+    frame fails with SQ_E_HIP "grid barrier timeout" instead of hanging; the
+    state stays the frame start, and the next frame without the switch is
+    bit-identical to a fresh context's."""
+    from stochquant_amd import Qm1dChain, StochQuantError
+    N, a, h, loops = 32768, 0.1, 0.01, 20
+    f, x, xx0 = _state(N, seed=4, amp=0.3)
+    om = N * a / 2
+    monkeypatch.setenv("SQ_QM1D_GRID", "1")
+    monkeypatch.setenv("SQ_QM1D_BAR_POLLS", str(1 << 16))
+    with Qm1dChain(N, a, h, pot=0, C=1.0, loops=loops, seed=2, adapt_dtau=False) as q:
+        q.upload(f, x, xx0, om, 0)
+        monkeypatch.setenv("SQ_QM1D_BAR_SKIP", "3")
+        with pytest.raises(StochQuantError, match="grid barrier timeout"):
+            q.run_frame()
+        monkeypatch.delenv("SQ_QM1D_BAR_SKIP")
+        d = q.download()
+        assert np.array_equal(d["f"], f) and np.array_equal(d["x"], x)
+        q.set_scan(0, 0.0, 0)
+        stable = q.run_frame()
+        got = q.download()
+    s_ref, ref, _ = _gpu_frame(N, a, h, 0, 1.0, loops, 2, f, x, xx0, om)
+    assert stable == s_ref
+    for k in ("f", "x", "xx0"):
+        assert np.array_equal(got[k], ref[k]), k

@@ -226,3 +226,32 @@ def test_taumain_driver_double_well(gpu, tmp_path):
     assert np.all(np.isfinite(y) | np.isneginf(y))   # -inf while no frame was stable yet (Δτ/Δt² = 5)
     assert frames[-1]["dtau"] <= 0.002
     assert (tmp_path / "V0_2e_0-8.txt").exists()
+
+
+@pytest.mark.parametrize("C", ["1", "0"])
+def test_configs0_phi4_32_through_tauhost(gpu, oracle_mod, tmp_path, C):
+    """BASELINE configs[0] read literally: a 32^3 scalar
+    φ⁴ lattice, Δτ = 0.01, 1000 Langevin steps through tauhost.o driven by
+    taumain.py's 13-argument argv (one frame of loops = 1000; SQ_MODEL=phi4,
+    SQ_SHAPE=32x32x32).  The end-file field equals the library run of the same
+    frame bit for bit; with the noise off (C = 0) it equals the CPU oracle's
+    1000 steps from the same start field bit for bit."""
+    from stochquant_amd import Phi4Lattice, tauhost_argv
+    env = dict(SQ_MODEL="phi4", SQ_SHAPE="32x32x32", SQ_SEED="24301")
+    argv = tauhost_argv(32, 1.0, 0.01, 1, 0, C, 0, 1, 0, 1000, "0", "END", 16)[1:]
+    out, _ = _run_env(tmp_path, argv, **env)
+    assert len(out.strip().split("\n")) == 1
+    cli = np.load(tmp_path / "end")
+    assert cli.shape == (32, 32, 32)
+    with Phi4Lattice((32, 32, 32), dtau=0.01, m2=1.0, lam=1.0, seed=24301, loops=1000, C=float(C)) as L:
+        L.init_field(float(np.float32(np.sqrt(2 * 0.01))))
+        phi0 = L.download()
+        assert L.run_frame()
+        lib = L.download()
+    assert np.array_equal(cli, lib)
+    if C == "0":
+        p = oracle_mod.phi4_params((32, 32, 32), 0.01, 1.0, 1.0, 24301, C=0.0)
+        ref = phi0
+        for s in range(1000):
+            ref = oracle_mod.phi4_step(p, ref, s)
+        assert np.array_equal(cli, ref), f"max diff {np.max(np.abs(cli - ref))}"
