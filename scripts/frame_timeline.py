@@ -47,6 +47,23 @@ def main():
           f"idle/frame {(t1 - t0 - busy) / 1e3 / nf:.1f} us")
     for n, d in by.most_common():
         print(f"  {d / 1e3 / nf:8.2f} us/frame  {cnt[n] / nf:5.2f} launches/frame  avg {d / cnt[n] / 1e3:7.2f} us  {n}")
+    # by the launch's index inside its frame (index 0 folds the previous frame's end)
+    # and the gap before it (the previous kernel's end to its start)
+    idx_d, idx_g = collections.defaultdict(list), collections.defaultdict(list)
+    prev_end = None
+    for j, (s, e, n) in enumerate(sel):
+        idx_d[j % a.per_frame].append((e - s) / 1e3)
+        if prev_end is not None:
+            idx_g[j % a.per_frame].append((s - prev_end) / 1e3)
+        prev_end = e
+    print("  launch index in frame: avg duration / avg gap before it (us)")
+    for i in sorted(idx_d):
+        g = idx_g.get(i) or [0.0]
+        print(f"    {i:2d}  {sum(idx_d[i]) / len(idx_d[i]):7.2f}  {sum(g) / len(g):6.2f}")
+    raw = [k for k in ks if "phi4_tb2" in k[2] and not is_frame(k[2]) and "<true," in k[2]]
+    if raw:
+        d = sorted((e - s) / 1e3 for s, e, _ in raw)
+        print(f"  raw instance: {len(raw)} launches, median {d[len(d) // 2]:.2f} us, mean {sum(d) / len(d):.2f} us")
 
 
 if __name__ == "__main__":

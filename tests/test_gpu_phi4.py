@@ -1102,4 +1102,6 @@ def test_launch_info_names_each_instance(gpu, monkeypatch):
     with _lat((32, 32, 32), dtau=0.01) as L:
         L.step(3)
         info = L.launch_info()
-        assert info["kernel"].startswith("phi4_step_kernel<32, ") and info["launches"] == 3, info
+        # 32-site rows: 8 lanes x 4 sites per row (QX = 8), one row per lane, packed-free scalar arithmetic
+        assert info["kernel"] == "phi4_step_kernel<8, 1, 1, false, true, 1, false>" and info["launches"] == 3, info
+        assert L.kernel_name.startswith(info["kernel"][:-len(", false>")] + ">"), (L.kernel_name, info)
