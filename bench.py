@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--cpu-seconds-c3", type=float, default=8.0, help="target wall time of the 512^3 CPU sample")
     ap.add_argument("--no-c1", action="store_true", help="skip the 32,768-site QM1D chain (configs[0]) sub-record")
     ap.add_argument("--c1-frames", type=int, default=8, help="timed 1000-step frames of the C1 chain")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the 1024^3 strong-scaling (configs[4]) sub-record, run at every N")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the frames_256 / slab_1gpu / c1_phi4_32 sub-records of the default run")
     ap.add_argument("--cpu-loops-c1", type=int, default=1000,
@@ -784,6 +786,48 @@ def c1_phi4_32_record(a, local):
             "stable": bool(stable), "tauhost_equals_library": bool(np.array_equal(fcli, flib))}
 
 
+def c5_record(a, world, rank, local, watch):
+    """BASELINE configs[4] / SURVEY §8d C5 in the same invocation: the 1024^3
+    lattice strong-scaled over the job's ranks (z-slabs, deep-halo exchange
+    overlapped with the interior on the second stream; one slab at N = 1),
+    timed like the headline (settle, warm-up, --steps, max over ranks), with
+    its own multi_rank_check and oracle_check against the committed digests
+    of 1024^3 at this N.  Collective: every rank runs it."""
+    import torch.distributed as dist
+    from stochquant_amd import verify
+    L5 = 1024
+    shape = (L5, L5, L5)
+    lat, slab_path = make_lattice(a, shape, world, rank, local)
+    try:
+        lat.init_field(0.1)
+        t, perf, settle, ssteps = measure(a, lat, world, slab_path, watch)
+        sites_local = lat.nz_local * L5 * L5
+        rl, _, _ = roofline(a, lat, L5, world, slab_path, t, perf, 1, sites_local)
+        checks = {}
+        for key, fn, cmp in (("multi_rank_check", verify.run_protocol, verify.check),
+                             ("oracle_check", verify.run_oracle_protocol, verify.oracle_check)):
+            d = fn(lat)
+            digests = [None] * world
+            if world > 1:
+                dist.all_gather_object(digests, d)
+            else:
+                digests = [d]
+            checks[key] = cmp(digests, shape, world)
+        ghost = lat.ghost[0] if slab_path else None
+        schedule = lat.schedule if slab_path else None
+        nz_local = lat.nz_local
+    finally:
+        lat.close()
+    value = float(L5 ** 3) * a.steps / t
+    return {"config": {"workload": f"phi^4 3-D Langevin step, 1024^3 fp32 split over {world} GPU(s) (BASELINE "
+                                   f"configs[4], strong scaling)", "lattice": list(shape),
+                       "per_gpu": [L5, L5, nz_local], "ghost_depth": ghost, "block_schedule": schedule,
+                       "dtau": a.dtau, "m2": 1.0, "lambda": 1.0},
+            "value": value, "unit": "site-updates/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "settle_ms": round(settle, 1), "settle_steps": ssteps, "ms_per_step": t * 1e3 / a.steps,
+            "scaling": "strong", "roofline": rl, **checks}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -946,6 +990,9 @@ def run(a, world, rank, watch):
             out["cpu_baseline"] = cpu_baseline(L, a.dtau, a.cpu_seconds)
         else:
             out["cpu_baseline"] = None
+    # the headline is complete: from here on a deadline or a hang in an optional
+    # sub-record prints this line (marked incomplete) instead of an error line
+    watch.set_partial(out if rank == 0 else {})
     # config C3 (BASELINE configs[2], 512^3 on one GPU) in the same invocation:
     # the same settle, warm-up and --steps, its own roofline and CPU sample
     if world == 1 and not a.strong and a.comm == "auto" and L == 256 and not a.no_c3:
@@ -986,6 +1033,15 @@ def run(a, world, rank, watch):
                 out[key] = fn(a, local)
             except Exception as e:  # the headline record stands without it
                 out[key] = {"error": str(e)[:300]}
+    # config C5 (BASELINE configs[4]): 1024^3 strong-scaled over the same ranks
+    if not a.strong and a.comm == "auto" and L == 256 and not a.no_c5:
+        watch.phase("c5_1024")
+        try:
+            c5 = c5_record(a, world, rank, local, watch)
+        except Exception as e:  # the headline record stands without it
+            c5 = {"error": str(e)[:300]}
+        if out is not None:
+            out["c5_1024"] = c5
     if world > 1:
         watch.phase("teardown")
         dist.barrier()

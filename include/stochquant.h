@@ -173,6 +173,11 @@ int sq_upload_field(sq_ctx *ctx, const float *phi, size_t count);
 int sq_download_field(sq_ctx *ctx, float *phi, size_t count);
 /* PHI4: phi = amp * Philox normal(seed, stream 2, site), generated on device. */
 int sq_init_field(sq_ctx *ctx, float amp);
+/* PHI4: phi = amp * (h - 2^23) / 2^23, h = the top 24 bits of splitmix64(i ^ key)
+ * for global site index i = (z Ly + y) Lx + x: a field any host reproduces
+ * bit for bit without the device's RNG (bench.py's oracle_check starts the
+ * noise-off parity protocol from it).  Collective like sq_init_field. */
+int sq_init_field_hash(sq_ctx *ctx, double amp, unsigned long long key);
 /* PHI4 local slab geometry: nz_local and the global z of its first plane. */
 int sq_slab(sq_ctx *ctx, long long *nz_local, long long *z0);
 /* PHI4 register tile of the step kernel: out = {lanes per x segment, rows

@@ -104,6 +104,7 @@ SIGNATURES = {
     "sq_upload_field": (ctypes.c_int, [_P, _F, ctypes.c_size_t]),
     "sq_download_field": (ctypes.c_int, [_P, _F, ctypes.c_size_t]),
     "sq_init_field": (ctypes.c_int, [_P, ctypes.c_float]),
+    "sq_init_field_hash": (ctypes.c_int, [_P, ctypes.c_double, ctypes.c_ulonglong]),
     "sq_slab": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_longlong), ctypes.POINTER(ctypes.c_longlong)]),
     "sq_moments": (ctypes.c_int, [_P, _D]),
     "sq_phi4_tile": (ctypes.c_int, [_P, _I]),

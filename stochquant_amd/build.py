@@ -28,7 +28,7 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("SQ_OFFLOAD_ARCH", "gfx950")
 
-DEVICE_SOURCES = ["sq_phi4.hip", "sq_qm1d.hip", "sq_qm1d_gs.hip", "sq_selftest.hip", "sq_p2p.hip"]
+DEVICE_SOURCES = ["sq_phi4.hip", "sq_qm1d.hip", "sq_qm1d_gs.hip", "sq_selftest.hip", "sq_p2p.hip", "sq_fields.hip"]
 HOST_SOURCES = ["sq_api.cpp", "sq_io.cpp"]
 HEADERS = ["sq_internal.h", "sq_rng.h", "sq_dpp.h", "sq_glibcf.h"]
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall",

@@ -2534,6 +2534,20 @@ int sq_init_field(sq_ctx *c, float amp) {
     return phi4_join(c);
 }
 
+int sq_init_field_hash(sq_ctx *c, double amp, unsigned long long key) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    if (!std::isfinite(amp) || std::fabs(amp) > 1e30) return fail(SQ_E_ARG, "amp must be finite");
+    DeviceGuard g(c->dev);
+    int rc = phi4_join(c);
+    if (rc) return rc;
+    for (auto &s : c->slabs)
+        SQ_HIP(sq::phi4_init_hash_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, key, amp, s.sA));
+    c->field_finite = std::fabs(amp) < c->p.clamp;  // |phi| <= |amp| < clamp: every site finite and unclamped
+    c->fin_sync = true;
+    return phi4_join(c);
+}
+
 int sq_moments(sq_ctx *c, double out[3]) {
     if (!c || !out) return fail(SQ_E_ARG, "null argument");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");

@@ -204,6 +204,10 @@ void phi4_fill_units(Phi4StepArgs &a, const Phi4Geom &g);
 hipError_t phi4_step_launch(const Phi4StepArgs &a, const Phi4Geom &g, hipStream_t s,
                             hipEvent_t start = nullptr, hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
 // slab = local plane 0 (past the ghost zone)
+// phi = amp * (top 24 bits of splitmix64(global index ^ key) - 2^23) / 2^23
+// (sq_fields.hip; the host restatement is stochquant_amd/verify.py hash_field)
+hipError_t phi4_init_hash_launch(float *slab, int Lx, int Ly, int nz, long long zg0, unsigned long long key,
+                                 double amp, hipStream_t s);
 hipError_t phi4_init_launch(float *slab, int Lx, int Ly, int nz, long long zg0, uint32_t k0,
                             uint32_t k1, float amp, hipStream_t s);
 // Moments of a slab: acc = {sum phi, sum phi^2}, acc_max = {bits(max |phi|),

@@ -261,6 +261,10 @@ class Phi4Lattice(_Ctx):
     def init_field(self, amp):
         _lib.call("sq_init_field", self._h, float(amp))
 
+    def init_field_hash(self, amp, key):
+        """phi = amp * (top 24 bits of splitmix64(global index ^ key) - 2^23) / 2^23 (sq_init_field_hash)."""
+        _lib.call("sq_init_field_hash", self._h, float(amp), int(key))
+
     def moments(self):
         out = np.zeros(3)
         _lib.call("sq_moments", self._h, _dptr(out))

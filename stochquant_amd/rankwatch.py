@@ -59,6 +59,7 @@ class Watch:
         os.makedirs(self.dir, exist_ok=True)
         self.t0 = time.time()
         self.phase_name = None
+        self.partial = None      # rank 0: the bench line once its headline part is complete (set_partial)
         self.done = threading.Event()
         self.on_expire = on_expire or self._expire
         self.phase("start")
@@ -75,6 +76,21 @@ class Watch:
             json.dump(rec, fh)
         os.replace(tmp, os.path.join(self.dir, f"rank{self.rank}.json"))
 
+    def set_partial(self, line):
+        """The run's line with its headline complete (a dict, still growing as
+        the optional sub-records are added).  From here on a deadline or a
+        SIGTERM prints it, marked incomplete, instead of the error line, and
+        the rank exits 0: a hang in an optional sub-record (a second
+        communicator, the 1024^3 strong-scaling record) does not cost the
+        headline."""
+        self.partial = line
+
+    def _print_partial(self, why):
+        d = dict(self.partial)
+        d["incomplete"] = {"phase": self.phase_name, "why": why,
+                           "rank_phases": read_phases(self.dir, self.world)}
+        print(json.dumps(d), flush=True)
+
     def fail(self, exc):
         """This rank raised: record it for the others' reports; rank 0 prints the line."""
         msg = f"{type(exc).__name__}: {exc}"[:400]
@@ -90,11 +106,14 @@ class Watch:
         import signal
 
         def handler(signum, frame):
+            why = f"rank {self.rank} terminated (signal {signum}) in phase '{self.phase_name}'"
             if not self.done.is_set():
                 self.done.set()
+                if self.partial is not None:
+                    self._print_partial(why)
+                    os._exit(0)
                 print(error_line(self.metric, self.world, self.deadline_s, read_phases(self.dir, self.world),
-                                 f"rank {self.rank} terminated (signal {signum}) in phase '{self.phase_name}'"),
-                      flush=True)
+                                 why), flush=True)
             os._exit(128 + signum)
         if self.rank == 0:
             signal.signal(signal.SIGTERM, handler)
@@ -109,6 +128,11 @@ class Watch:
         self.on_expire(self)
 
     def _expire(self, _self):
+        if self.partial is not None:
+            # rank 0 holds the completed headline: print it, every rank exits 0
+            if self.rank == 0:
+                self._print_partial(f"rank deadline of {self.deadline_s:.0f} s passed in an optional sub-record")
+            os._exit(0)
         if self.rank == 0:
             phases = read_phases(self.dir, self.world)
             print(error_line(self.metric, self.world, self.deadline_s, phases,

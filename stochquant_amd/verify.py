@@ -91,14 +91,14 @@ def load_oracle_golden(path=ORACLE_GOLDEN):
 
 def run_oracle_protocol(lat, corrupt=False):
     """The noise-off parity protocol (collective in multi-rank contexts): C = 0,
-    this rank's slab of hash_field uploaded, the step counter at 0,
+    this rank's slab of hash_field (sq_init_field_hash, on the device), the step counter at 0,
     CHECK_STEPS steps; returns the slab digest.  With the noise off the step is
     deterministic fp32 arithmetic, so the digest must equal the oracle's
     (oracle/orc_phi4.c, tests/golden/make_oracle_slabs.py) bit for bit."""
     C0 = float(lat.params.C)
     lat.set_noise(0.0)
     try:
-        lat.upload(hash_field(lat.shape, lat.z0, lat.nz_local))
+        lat.init_field_hash(HASH_FIELD_AMP, HASH_FIELD_KEY)   # = hash_field, generated on the device
         lat.step_counter = 0
         lat.step(CHECK_STEPS)
         f = lat.download()

@@ -121,3 +121,33 @@ def test_two_ranks_on_one_gpu_default_transport():
         assert "(p2p)" in par
     else:
         assert "(rccl)" in par
+
+
+def test_deadline_after_the_headline_prints_the_partial_line(tmp_path):
+    """Once the headline is complete (Watch.set_partial), a deadline in an
+    optional sub-record prints that line marked "incomplete" and every rank
+    exits 0 -- a hang in, e.g., the 1024^3 strong-scaling record does not cost
+    the headline; before it, the error line and exit 3 as before."""
+    import subprocess
+    import sys
+    code = ("import sys, time, json; sys.path.insert(0, %r)\n"
+            "from stochquant_amd import rankwatch\n"
+            "w = rankwatch.Watch(int(sys.argv[1]), 2, 2.0, 'm', d=%r)\n"
+            "if sys.argv[2] == '1': w.set_partial({'metric': 'm', 'value': 1.5} if sys.argv[1] == '0' else {})\n"
+            "w.phase('c5_1024')\n"
+            "time.sleep(30)\n") % (ROOT, str(tmp_path))
+    for rank in ("0", "1"):
+        for partial in ("1", "0"):
+            r = subprocess.run([sys.executable, "-c", code, rank, partial], capture_output=True, text=True, timeout=60)
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if partial == "1":
+                assert r.returncode == 0, r.stderr
+                if rank == "0":
+                    d = json.loads(lines[0])
+                    assert d["value"] == 1.5 and d["incomplete"]["phase"] == "c5_1024", d
+                else:
+                    assert lines == []
+            else:
+                assert r.returncode == 3
+                if rank == "0":
+                    assert json.loads(lines[0])["value"] is None

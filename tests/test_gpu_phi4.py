@@ -1105,3 +1105,20 @@ def test_launch_info_names_each_instance(gpu, monkeypatch):
         # 32-site rows: 8 lanes x 4 sites per row (QX = 8), one row per lane, packed-free scalar arithmetic
         assert info["kernel"] == "phi4_step_kernel<8, 1, 1, false, true, 1, false>" and info["launches"] == 3, info
         assert L.kernel_name.startswith(info["kernel"][:-len(", false>")] + ">"), (L.kernel_name, info)
+
+
+@pytest.mark.parametrize("shape,kw", [((256, 16, 24), {}), ((32, 8, 13), {}), ((256, 8, 30), {"comm": "loopback", "nslabs": 4}),
+                                      ((64, 16, 12), {"comm": "rccl"})])
+def test_init_field_hash_matches_host(gpu, shape, kw):
+    """sq_init_field_hash on the device is verify.hash_field (numpy) bit for
+    bit, slab by slab: the oracle's digests start from the same field."""
+    from stochquant_amd import unique_id, verify
+    if kw.get("comm") == "rccl":
+        kw = dict(kw, nranks=1, rank=0, comm_id=unique_id())
+    with _lat(shape, **kw) as L:
+        L.init_field_hash(verify.HASH_FIELD_AMP, verify.HASH_FIELD_KEY)
+        got = L.download()
+        L.init_field_hash(0.5, 12345)
+        other = L.download()
+    assert np.array_equal(got, verify.hash_field(shape, 0, shape[2]))
+    assert not np.array_equal(other, got) and np.abs(other).max() <= 0.5
