@@ -633,7 +633,60 @@ __device__ __forceinline__ bool grid_barrier(unsigned int *ctr, unsigned int n, 
     return s_ok != 0;
 }
 
-template <int kGridK>
+// The hand-off without cache maintenance (SC1 = true, the default; DESIGN.md
+// §4): every byte one block writes for another -- the field's sites, X' by
+// parity, the block maxima -- is stored with an sc1 store (write-through, the
+// line dropped from the writer's L2) and every load of such bytes is an sc1
+// load (it bypasses the reader's L1), so the barrier needs neither the
+// release's L2 write-back (buffer_wbl2) nor the acquire's L1 invalidate
+// (buffer_inv): every wave waits for its own stores (s_waitcnt vmcnt(0)), the
+// block meets at a barrier, one lane adds to the counter (a relaxed agent
+// atomic) and polls it with relaxed sc1 loads, and the block follows through
+// a second barrier (MI355X_MICROARCH.md "Valid forms": one lane signals for
+// its workgroup, sc1 stores and loads of 8 B, hipMalloc memory).  The acquire
+// form (SC1 = false, SQ_QM1D_BAR=1) keeps release / acquire fences around a
+// counter polled with acquire loads: each poll and each fence is an L2
+// write-back or L1 invalidate of ~1.7 us, about 9 us per step at N = 32,768.
+// (global address space explicitly: a pointer picked from a local array, as
+// Xb[par], otherwise becomes a flat access, and the hand-off is measured for
+// global_ / buffer_ sc1 accesses)
+typedef __attribute__((address_space(1))) double gdouble;
+template <bool SC1>
+__device__ __forceinline__ double ld_x(const double *p) {
+    if constexpr (SC1)
+        return __hip_atomic_load((const gdouble *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void st_x(double *p, double v) {
+    if constexpr (SC1) __hip_atomic_store((gdouble *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+__device__ __forceinline__ bool grid_barrier_sc1(unsigned int *ctr, unsigned int n, int *err, unsigned int polls,
+                                                 bool skip) {
+    __shared__ int s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores (and atomics) have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!skip) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int target = n * gridDim.x;
+        int ok = 1;
+        for (unsigned int k = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++k) {
+            if (k >= polls ||
+                ((k & 1023u) == 1023u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+template <int kGridK, bool SC1>
 __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     cooperative_groups::grid_group grid = cooperative_groups::this_grid();
     unsigned int *bar = reinterpret_cast<unsigned int *>(A.ds + A.N) + 4;  // zeroed before the launch
@@ -647,9 +700,9 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     double *Xb[2] = {A.xs, A.ds};
     double *bm = A.xs + N;  // [parity][X | A][G]
     unsigned long long *lead = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lead + 1;
-    if (gt == 0) {
-        *lead = 0ull;
-        *unst = 0ull;
+    if (gt == 0) {  // write-through (agent scope): the other blocks' atomics and sc1 loads must see the zeros
+        __hip_atomic_store(lead, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(unst, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     double nx[kGridK], nxx0[kGridK], D[kGridK];
 #pragma unroll
@@ -672,16 +725,16 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             // 1. site updates of step j
             const unsigned long long step = A.tick + (unsigned long long)j;
             const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-            const double Xm = fin[mid] + xcl((double)mid * a, om, pot);
+            const double Xm = ld_x<SC1>(fin + mid) + xcl((double)mid * a, om, pot);
             const double den = (double)(A.runs + j + 1);
             double lmaxX = -INFINITY, lmaxA = -INFINITY;
             if (own > 0) {
                 f32x4n nq = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
                 double fc[kGridK];
 #pragma unroll
-                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
-                const double fL = i0 > 0 ? fin[i0 - 1] : 0.;
-                const double fR = i0 + own < N ? fin[i0 + own] : 0.;
+                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? ld_x<SC1>(fin + i0 + k) : 0.;
+                const double fL = i0 > 0 ? ld_x<SC1>(fin + i0 - 1) : 0.;
+                const double fR = i0 + own < N ? ld_x<SC1>(fin + i0 + own) : 0.;
 #pragma unroll
                 for (int k = 0; k < kGridK; ++k) {
                     if (k >= own) break;
@@ -714,8 +767,8 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     const double Xi = fi + xc;
                     nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
                     nx[k] = nx[k] + (Xi - nx[k]) / den;
-                    fout[i] = v;
-                    Xb[par][i] = X[k];
+                    st_x<SC1>(fout + i, v);
+                    st_x<SC1>(Xb[par] + i, X[k]);
                 }
             }
             ix = wave_incl_max(lmaxX, lane);
@@ -731,21 +784,27 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     bx = fmax(bx, s_wX[par][w]);
                     ba = fmax(ba, s_wA[par][w]);
                 }
-                bm[(2 * par) * G + b] = bx;
-                bm[(2 * par + 1) * G + b] = ba;
+                st_x<SC1>(bm + (2 * par) * G + b, bx);
+                st_x<SC1>(bm + (2 * par + 1) * G + b, ba);
             }
         }
-        if (A.gbar) {
-            if (!grid_barrier(bar, (unsigned int)(j + 1), &A.st->sync_error, A.bar_polls ? A.bar_polls : kGridSpinMax,
-                              j == 0 && b == A.bar_skip))
+        if constexpr (SC1) {
+            if (!grid_barrier_sc1(bar, (unsigned int)(j + 1), &A.st->sync_error,
+                                  A.bar_polls ? A.bar_polls : kGridSpinMax, j == 0 && b == A.bar_skip))
                 return;  // a barrier gave up: the frame is void (the host reports it)
         } else {
-            grid.sync();
+            if (A.gbar) {
+                if (!grid_barrier(bar, (unsigned int)(j + 1), &A.st->sync_error,
+                                  A.bar_polls ? A.bar_polls : kGridSpinMax, j == 0 && b == A.bar_skip))
+                    return;
+            } else {
+                grid.sync();
+            }
+            // acquire only: every block's writes before the barrier were released by
+            // its thread 0 (after the block's __syncthreads) -- a full __threadfence
+            // here made every wave write back the L2 again each step
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        // acquire only: every block's writes before the barrier were released by
-        // its thread 0 (after the block's __syncthreads) -- a full __threadfence
-        // here made every wave write back the L2 again each step
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
@@ -760,10 +819,10 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         }
         if (j == A.loops) break;
         // 2b. step j's ordered scan
-        double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
+        double runX = (E >= 0 && E < N) ? ld_x<SC1>(Xb[par] + E) : -INFINITY, runA = V;
         totA = V;
         for (int q = 0; q < G; ++q) {
-            const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
+            const double qx = ld_x<SC1>(bm + (2 * par) * G + q), qa = ld_x<SC1>(bm + (2 * par + 1) * G + q);
             if (q < b) {
                 runX = fmax(runX, qx);
                 runA = fmax(runA, qa);
@@ -810,7 +869,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
 #pragma unroll
     for (int k = 0; k < kGridK; ++k) {
         if (k >= own) break;
-        if (fin != A.nf) A.nf[i0 + k] = fin[i0 + k];
+        if (fin != A.nf) A.nf[i0 + k] = ld_x<SC1>(fin + i0 + k);
         A.nx[i0 + k] = nx[k];
         A.nxx0[i0 + k] = nxx0[k];
     }
@@ -900,7 +959,7 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         // the counter barrier: N = 32,768 10.8 vs 11.7 ms per 1000-step frame with
         // cooperative groups' grid.sync (profiles/r03/qm1d_grid/); SQ_QM1D_BAR=0
         const char *gb = getenv("SQ_QM1D_BAR");
-        q.gbar = gb ? atoi(gb) : 1;
+        q.gbar = gb ? atoi(gb) : 2;
         // tests: a block that never arrives (SQ_QM1D_BAR_SKIP=b) and a shorter poll budget
         const char *bs = getenv("SQ_QM1D_BAR_SKIP"), *bp = getenv("SQ_QM1D_BAR_POLLS");
         q.bar_skip = bs ? atoi(bs) : -1;
@@ -910,11 +969,13 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         void *args[] = {&q};
-        const void *fn = kk == 2    ? (const void *)qm1d_frame_grid<2>
-                         : kk == 8  ? (const void *)qm1d_frame_grid<8>
-                         : kk == 16 ? (const void *)qm1d_frame_grid<16>
-                         : kk == 32 ? (const void *)qm1d_frame_grid<32>
-                                    : (const void *)qm1d_frame_grid<4>;
+        // SQ_QM1D_BAR=2 (default): the sc1 hand-off barrier; 1: release / acquire
+        // fences around the counter; 0: cooperative groups' grid.sync
+        const bool sc1 = q.gbar == 2;
+#define SQ_GRIDK(K) (sc1 ? (const void *)qm1d_frame_grid<K, true> : (const void *)qm1d_frame_grid<K, false>)
+        const void *fn = kk == 2 ? SQ_GRIDK(2) : kk == 8 ? SQ_GRIDK(8) : kk == 16 ? SQ_GRIDK(16)
+                                                          : kk == 32 ? SQ_GRIDK(32) : SQ_GRIDK(4);
+#undef SQ_GRIDK
         if (q.gbar) {
             // the counter barrier needs every block resident, not the
             // cooperative-launch machinery (GWS, its own queue); a plain launch

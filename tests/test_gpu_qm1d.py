@@ -203,20 +203,23 @@ def test_large_chain_double_well_within_tolerance(gpu, oracle_mod):
         assert np.max(np.abs(d[k] - r[k])) <= tol
 
 
+@pytest.mark.parametrize("bar", ["2", "1", "0"])
 @pytest.mark.parametrize("N,pot,C,h", [(8192, 3, 1.0, 0.002), (32768, 0, 1.0, 0.01), (65536, 3, 1.0, 0.002),
                                        (4097, 0, 1.0, 0.002), (20000, 3, 1.0, 0.09)])
-def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h):
-    """N > 4096: the cooperative multi-block frame (qm1d_frame_grid, two grid
-    barriers per step) and the one-work-group frame (SQ_QM1D_GRID=0) are
-    bit-identical with the noise on: field, running means, omega, the carried
-    scan state and the verdict -- incl. a step size that makes the frame
-    unstable part-way (last case)."""
+def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
+    """N > 4096: the multi-block frame (qm1d_frame_grid, one grid barrier per
+    step) and the one-work-group frame (SQ_QM1D_GRID=0) are bit-identical with
+    the noise on: field, running means, omega, the carried scan state and the
+    verdict -- incl. a step size that makes the frame unstable part-way (last
+    case).  Every barrier form: the sc1 hand-off (SQ_QM1D_BAR=2, the default),
+    release / acquire fences around the counter (1), cooperative groups (0)."""
     a, loops = 0.1, 40
     f, x, xx0 = _state(N, seed=11, amp=0.3)
     om = N * a / 2 + 0.013
 
     def run(grid):
         monkeypatch.setenv("SQ_QM1D_GRID", grid)
+        monkeypatch.setenv("SQ_QM1D_BAR", bar)
         return _gpu_frame(N, a, h, pot, C, loops, 5, f, x, xx0, om, runs=3, lrgEl=N // 3, lrgVl=0.2, tick=11)
 
     s1, d1, c1 = run("1")
@@ -255,3 +258,29 @@ def test_grid_barrier_timeout_returns_error(gpu, monkeypatch):
     assert stable == s_ref
     for k in ("f", "x", "xx0"):
         assert np.array_equal(got[k], ref[k]), k
+
+
+def test_grid_sc1_handoff_c1_frames_bitwise(gpu, monkeypatch):
+    """Config C1 itself (N = 32,768, Δτ = 0.01, potID 0, C = 1, 1000-step
+    frames), two frames back to back: the sc1 hand-off barrier (the default),
+    the fenced counter barrier and the one-work-group kernel give the same bits
+    -- 2,000 grid barriers, each a chance for a stale neighbour site, block
+    maximum or X' to show up."""
+    from stochquant_amd import Qm1dChain
+    N, a, h, loops = 32768, 1.0, 0.01, 1000
+    f0 = np.sqrt(2 * h) * np.random.default_rng(1).standard_normal(N)
+
+    def run(grid, bar):
+        monkeypatch.setenv("SQ_QM1D_GRID", grid)
+        monkeypatch.setenv("SQ_QM1D_BAR", bar)
+        with Qm1dChain(N, a, h, pot=0, C=1.0, loops=loops, seed=1) as q:
+            q.upload(f0, omega=a * (N // 2))
+            st = [q.run_frame() for _ in range(2)]
+            return st, q.download(), q.scan
+    ref = run("0", "1")
+    for grid, bar in (("1", "2"), ("1", "1")):
+        got = run(grid, bar)
+        assert got[0] == ref[0], (bar, got[0], ref[0])
+        for k in ("f", "x", "xx0"):
+            assert np.array_equal(got[1][k], ref[1][k]), (bar, k)
+        assert got[1]["omega"] == ref[1]["omega"] and got[2] == ref[2], bar
