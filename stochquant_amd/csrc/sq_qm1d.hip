@@ -633,60 +633,53 @@ __device__ __forceinline__ bool grid_barrier(unsigned int *ctr, unsigned int n, 
     return s_ok != 0;
 }
 
-// The hand-off without cache maintenance (SC1 = true, the default; DESIGN.md
-// §4): every byte one block writes for another -- the field's sites, X' by
-// parity, the block maxima -- is stored with an sc1 store (write-through, the
-// line dropped from the writer's L2) and every load of such bytes is an sc1
-// load (it bypasses the reader's L1), so the barrier needs neither the
-// release's L2 write-back (buffer_wbl2) nor the acquire's L1 invalidate
-// (buffer_inv): every wave waits for its own stores (s_waitcnt vmcnt(0)), the
-// block meets at a barrier, one lane adds to the counter (a relaxed agent
-// atomic) and polls it with relaxed sc1 loads, and the block follows through
-// a second barrier (MI355X_MICROARCH.md "Valid forms": one lane signals for
-// its workgroup, sc1 stores and loads of 8 B, hipMalloc memory).  The acquire
-// form (SC1 = false, SQ_QM1D_BAR=1) keeps release / acquire fences around a
-// counter polled with acquire loads: each poll and each fence is an L2
-// write-back or L1 invalidate of ~1.7 us, about 9 us per step at N = 32,768.
-// (global address space explicitly: a pointer picked from a local array, as
-// Xb[par], otherwise becomes a flat access, and the hand-off is measured for
-// global_ / buffer_ sc1 accesses)
-typedef __attribute__((address_space(1))) double gdouble;
-template <bool SC1>
-__device__ __forceinline__ double ld_x(const double *p) {
-    if constexpr (SC1)
-        return __hip_atomic_load((const gdouble *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-template <bool SC1>
-__device__ __forceinline__ void st_x(double *p, double v) {
-    if constexpr (SC1) __hip_atomic_store((gdouble *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
-__device__ __forceinline__ bool grid_barrier_sc1(unsigned int *ctr, unsigned int n, int *err, unsigned int polls,
-                                                 bool skip) {
+// The same barrier without a shared counter (SQ_QM1D_BAR=3): every block
+// publishes its arrival in its own flag word (64 B apart) -- lane 0, behind the
+// block's stores, a release fence and a relaxed store -- and wave 0 polls all
+// G flags in parallel with relaxed loads (lane l the blocks l, l+64, ...)
+// until every one has reached barrier n, then one acquire fence for the CU.
+// The counter barrier's atomic adds queue on one address (≈0.35 us per block
+// and step: C1 per-step time grows by that much per block, SQ_QM1D_GK
+// 8 / 4 / 2 = 16 / 32 / 64 blocks, profiles/r03/qm1d_grid/), and it polls with
+// acquire loads (an L1 invalidate per poll); flags cost one store per block.
+// Bounded like grid_barrier.
+__device__ __forceinline__ bool grid_barrier_flags(unsigned int *flags, unsigned int n, int *err,
+                                                   unsigned int polls, bool skip) {
     __shared__ int s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores (and atomics) have landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores have left
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (!skip) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned int target = n * gridDim.x;
+    if (threadIdx.x < 64) {
+        const int lane = (int)threadIdx.x, G = (int)gridDim.x;
+        if (lane == 0 && !skip) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the block's writes, past the XCD's L2
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(flags + 16 * blockIdx.x, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         int ok = 1;
-        for (unsigned int k = 0; __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++k) {
+        for (unsigned int k = 0;; ++k) {
+            bool mine = true;
+            for (int q = lane; q < G; q += 64)
+                mine = mine && __hip_atomic_load(flags + 16 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= n;
+            if (__all(mine)) break;
             if (k >= polls ||
                 ((k & 1023u) == 1023u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)) {
-                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ok = 0;
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        s_ok = ok;
+        if (ok) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1: the other blocks' writes
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        if (lane == 0) s_ok = ok;
     }
     __syncthreads();
     return s_ok != 0;
 }
 
-template <int kGridK, bool SC1>
+template <int kGridK>
 __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     cooperative_groups::grid_group grid = cooperative_groups::this_grid();
     unsigned int *bar = reinterpret_cast<unsigned int *>(A.ds + A.N) + 4;  // zeroed before the launch
@@ -700,9 +693,9 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     double *Xb[2] = {A.xs, A.ds};
     double *bm = A.xs + N;  // [parity][X | A][G]
     unsigned long long *lead = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lead + 1;
-    if (gt == 0) {  // write-through (agent scope): the other blocks' atomics and sc1 loads must see the zeros
-        __hip_atomic_store(lead, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(unst, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (gt == 0) {
+        *lead = 0ull;
+        *unst = 0ull;
     }
     double nx[kGridK], nxx0[kGridK], D[kGridK];
 #pragma unroll
@@ -725,16 +718,16 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             // 1. site updates of step j
             const unsigned long long step = A.tick + (unsigned long long)j;
             const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-            const double Xm = ld_x<SC1>(fin + mid) + xcl((double)mid * a, om, pot);
+            const double Xm = fin[mid] + xcl((double)mid * a, om, pot);
             const double den = (double)(A.runs + j + 1);
             double lmaxX = -INFINITY, lmaxA = -INFINITY;
             if (own > 0) {
                 f32x4n nq = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
                 double fc[kGridK];
 #pragma unroll
-                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? ld_x<SC1>(fin + i0 + k) : 0.;
-                const double fL = i0 > 0 ? ld_x<SC1>(fin + i0 - 1) : 0.;
-                const double fR = i0 + own < N ? ld_x<SC1>(fin + i0 + own) : 0.;
+                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
+                const double fL = i0 > 0 ? fin[i0 - 1] : 0.;
+                const double fR = i0 + own < N ? fin[i0 + own] : 0.;
 #pragma unroll
                 for (int k = 0; k < kGridK; ++k) {
                     if (k >= own) break;
@@ -767,8 +760,8 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     const double Xi = fi + xc;
                     nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
                     nx[k] = nx[k] + (Xi - nx[k]) / den;
-                    st_x<SC1>(fout + i, v);
-                    st_x<SC1>(Xb[par] + i, X[k]);
+                    fout[i] = v;
+                    Xb[par][i] = X[k];
                 }
             }
             ix = wave_incl_max(lmaxX, lane);
@@ -784,18 +777,18 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     bx = fmax(bx, s_wX[par][w]);
                     ba = fmax(ba, s_wA[par][w]);
                 }
-                st_x<SC1>(bm + (2 * par) * G + b, bx);
-                st_x<SC1>(bm + (2 * par + 1) * G + b, ba);
+                bm[(2 * par) * G + b] = bx;
+                bm[(2 * par + 1) * G + b] = ba;
             }
         }
-        if constexpr (SC1) {
-            if (!grid_barrier_sc1(bar, (unsigned int)(j + 1), &A.st->sync_error,
-                                  A.bar_polls ? A.bar_polls : kGridSpinMax, j == 0 && b == A.bar_skip))
+        const unsigned int polls = A.bar_polls ? A.bar_polls : kGridSpinMax;
+        if (A.gbar == 3) {
+            if (!grid_barrier_flags(bar + 16, (unsigned int)(j + 1), &A.st->sync_error, polls,
+                                    j == 0 && b == A.bar_skip))
                 return;  // a barrier gave up: the frame is void (the host reports it)
         } else {
             if (A.gbar) {
-                if (!grid_barrier(bar, (unsigned int)(j + 1), &A.st->sync_error,
-                                  A.bar_polls ? A.bar_polls : kGridSpinMax, j == 0 && b == A.bar_skip))
+                if (!grid_barrier(bar, (unsigned int)(j + 1), &A.st->sync_error, polls, j == 0 && b == A.bar_skip))
                     return;
             } else {
                 grid.sync();
@@ -819,10 +812,10 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         }
         if (j == A.loops) break;
         // 2b. step j's ordered scan
-        double runX = (E >= 0 && E < N) ? ld_x<SC1>(Xb[par] + E) : -INFINITY, runA = V;
+        double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
         totA = V;
         for (int q = 0; q < G; ++q) {
-            const double qx = ld_x<SC1>(bm + (2 * par) * G + q), qa = ld_x<SC1>(bm + (2 * par + 1) * G + q);
+            const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
             if (q < b) {
                 runX = fmax(runX, qx);
                 runA = fmax(runA, qa);
@@ -869,7 +862,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
 #pragma unroll
     for (int k = 0; k < kGridK; ++k) {
         if (k >= own) break;
-        if (fin != A.nf) A.nf[i0 + k] = ld_x<SC1>(fin + i0 + k);
+        if (fin != A.nf) A.nf[i0 + k] = fin[i0 + k];
         A.nx[i0 + k] = nx[k];
         A.nxx0[i0 + k] = nxx0[k];
     }
@@ -959,23 +952,23 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         // the counter barrier: N = 32,768 10.8 vs 11.7 ms per 1000-step frame with
         // cooperative groups' grid.sync (profiles/r03/qm1d_grid/); SQ_QM1D_BAR=0
         const char *gb = getenv("SQ_QM1D_BAR");
-        q.gbar = gb ? atoi(gb) : 2;
+        q.gbar = gb ? atoi(gb) : 1;
         // tests: a block that never arrives (SQ_QM1D_BAR_SKIP=b) and a shorter poll budget
         const char *bs = getenv("SQ_QM1D_BAR_SKIP"), *bp = getenv("SQ_QM1D_BAR_POLLS");
         q.bar_skip = bs ? atoi(bs) : -1;
         q.bar_polls = bp ? (unsigned int)strtoul(bp, nullptr, 10) : 0u;
-        if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (after the tagged words)
-            hipError_t e = hipMemsetAsync(reinterpret_cast<unsigned int *>(q.ds + q.N) + 4, 0, sizeof(unsigned int), s);
+        if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (after the tagged words); the
+                       // flag barrier's G words 64 B apart after it (ds[N] + 80 bytes: < kQm1dGridAux doubles)
+            if (80 + 64 * (size_t)G > sizeof(double) * kQm1dGridAux) return hipErrorInvalidValue;
+            hipError_t e = hipMemsetAsync(reinterpret_cast<unsigned int *>(q.ds + q.N) + 4, 0, 64 + 64 * (size_t)G, s);
             if (e != hipSuccess) return e;
         }
         void *args[] = {&q};
-        // SQ_QM1D_BAR=2 (default): the sc1 hand-off barrier; 1: release / acquire
-        // fences around the counter; 0: cooperative groups' grid.sync
-        const bool sc1 = q.gbar == 2;
-#define SQ_GRIDK(K) (sc1 ? (const void *)qm1d_frame_grid<K, true> : (const void *)qm1d_frame_grid<K, false>)
-        const void *fn = kk == 2 ? SQ_GRIDK(2) : kk == 8 ? SQ_GRIDK(8) : kk == 16 ? SQ_GRIDK(16)
-                                                          : kk == 32 ? SQ_GRIDK(32) : SQ_GRIDK(4);
-#undef SQ_GRIDK
+        const void *fn = kk == 2    ? (const void *)qm1d_frame_grid<2>
+                         : kk == 8  ? (const void *)qm1d_frame_grid<8>
+                         : kk == 16 ? (const void *)qm1d_frame_grid<16>
+                         : kk == 32 ? (const void *)qm1d_frame_grid<32>
+                                    : (const void *)qm1d_frame_grid<4>;
         if (q.gbar) {
             // the counter barrier needs every block resident, not the
             // cooperative-launch machinery (GWS, its own queue); a plain launch

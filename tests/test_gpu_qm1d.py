@@ -203,7 +203,7 @@ def test_large_chain_double_well_within_tolerance(gpu, oracle_mod):
         assert np.max(np.abs(d[k] - r[k])) <= tol
 
 
-@pytest.mark.parametrize("bar", ["2", "1", "0"])
+@pytest.mark.parametrize("bar", ["3", "1", "0"])
 @pytest.mark.parametrize("N,pot,C,h", [(8192, 3, 1.0, 0.002), (32768, 0, 1.0, 0.01), (65536, 3, 1.0, 0.002),
                                        (4097, 0, 1.0, 0.002), (20000, 3, 1.0, 0.09)])
 def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
@@ -211,8 +211,8 @@ def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
     step) and the one-work-group frame (SQ_QM1D_GRID=0) are bit-identical with
     the noise on: field, running means, omega, the carried scan state and the
     verdict -- incl. a step size that makes the frame unstable part-way (last
-    case).  Every barrier form: the sc1 hand-off (SQ_QM1D_BAR=2, the default),
-    release / acquire fences around the counter (1), cooperative groups (0)."""
+    case).  Every barrier form: per-block flags (SQ_QM1D_BAR=3), release /
+    acquire fences around one counter (1), cooperative groups (0)."""
     a, loops = 0.1, 40
     f, x, xx0 = _state(N, seed=11, amp=0.3)
     om = N * a / 2 + 0.013
@@ -230,7 +230,8 @@ def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
     assert d1["omega"] == d0["omega"] and c1 == c0
 
 
-def test_grid_barrier_timeout_returns_error(gpu, monkeypatch):
+@pytest.mark.parametrize("bar", ["1", "3"])
+def test_grid_barrier_timeout_returns_error(gpu, monkeypatch, bar):
     """The grid kernel's counter barrier is bounded: with a
     debug switch one block never arrives at the first barrier
     (SQ_QM1D_BAR_SKIP), every block gives up after its poll budget, and the
@@ -242,6 +243,7 @@ def test_grid_barrier_timeout_returns_error(gpu, monkeypatch):
     f, x, xx0 = _state(N, seed=4, amp=0.3)
     om = N * a / 2
     monkeypatch.setenv("SQ_QM1D_GRID", "1")
+    monkeypatch.setenv("SQ_QM1D_BAR", bar)
     monkeypatch.setenv("SQ_QM1D_BAR_POLLS", str(1 << 16))
     with Qm1dChain(N, a, h, pot=0, C=1.0, loops=loops, seed=2, adapt_dtau=False) as q:
         q.upload(f, x, xx0, om, 0)
@@ -262,24 +264,25 @@ def test_grid_barrier_timeout_returns_error(gpu, monkeypatch):
 
 def test_grid_sc1_handoff_c1_frames_bitwise(gpu, monkeypatch):
     """Config C1 itself (N = 32,768, Δτ = 0.01, potID 0, C = 1, 1000-step
-    frames), two frames back to back: the sc1 hand-off barrier (the default),
-    the fenced counter barrier and the one-work-group kernel give the same bits
-    -- 2,000 grid barriers, each a chance for a stale neighbour site, block
-    maximum or X' to show up."""
+    frames), two frames back to back: the flag barrier, the counter barrier
+    and the one-work-group kernel give the same bits, at 8 and 2 sites per
+    thread (16 and 64 blocks) -- 2,000 grid barriers, each a chance for a
+    stale neighbour site, block maximum or X' to show up."""
     from stochquant_amd import Qm1dChain
     N, a, h, loops = 32768, 1.0, 0.01, 1000
     f0 = np.sqrt(2 * h) * np.random.default_rng(1).standard_normal(N)
 
-    def run(grid, bar):
+    def run(grid, bar, gk="8"):
         monkeypatch.setenv("SQ_QM1D_GRID", grid)
         monkeypatch.setenv("SQ_QM1D_BAR", bar)
+        monkeypatch.setenv("SQ_QM1D_GK", gk)
         with Qm1dChain(N, a, h, pot=0, C=1.0, loops=loops, seed=1) as q:
             q.upload(f0, omega=a * (N // 2))
             st = [q.run_frame() for _ in range(2)]
             return st, q.download(), q.scan
     ref = run("0", "1")
-    for grid, bar in (("1", "2"), ("1", "1")):
-        got = run(grid, bar)
+    for grid, bar, gk in (("1", "3", "8"), ("1", "1", "8"), ("1", "3", "2"), ("1", "3", "4")):
+        got = run(grid, bar, gk)
         assert got[0] == ref[0], (bar, got[0], ref[0])
         for k in ("f", "x", "xx0"):
             assert np.array_equal(got[1][k], ref[1][k]), (bar, k)
