@@ -1577,6 +1577,14 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     st.lrgEl = c->lrgEl;
     st.lrgVl = c->lrgVl;
     SQ_HIP(hipMemcpyAsync(c->qst, &st, sizeof st, hipMemcpyHostToDevice, c->qstream));
+    // diagnostics (SQ_QM1D_STAMPS=<path>, grid kernel): per-block phase stamps of
+    // the frame's first 64 steps, appended to <path> as text (block step t0..t4)
+    const char *dpath = getenv("SQ_QM1D_STAMPS");
+    const size_t ndbg = (size_t)sq::kQm1dMaxN / 512 * 64 * 5;  // up to 128 blocks
+    if (dpath && c->N > sq::kQm1dRegMaxN) {
+        SQ_HIP(hipMalloc(&a.dbg, ndbg * sizeof(unsigned long long)));
+        SQ_HIP(hipMemsetAsync(a.dbg, 0, ndbg * sizeof(unsigned long long), c->qstream));
+    }
     EvPair *e = nullptr;
     int rc = ev_begin(c, c->qstream, &e);
     if (rc) return rc;
@@ -1585,6 +1593,18 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     if (e) SQ_HIP(hipEventRecord(e->b, c->qstream));
     SQ_HIP(hipMemcpyAsync(&st, c->qst, sizeof st, hipMemcpyDeviceToHost, c->qstream));
     SQ_HIP(hipStreamSynchronize(c->qstream));
+    if (a.dbg) {
+        std::vector<unsigned long long> h(ndbg);
+        SQ_HIP(hipMemcpy(h.data(), a.dbg, ndbg * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        (void)hipFree(a.dbg);
+        if (FILE *fp = fopen(dpath, "a")) {
+            for (size_t q = 0; q < ndbg / 5; ++q)
+                if (h[5 * q])
+                    fprintf(fp, "%zu %zu %llu %llu %llu %llu %llu\n", q / 64, q % 64, h[5 * q], h[5 * q + 1],
+                            h[5 * q + 2], h[5 * q + 3], h[5 * q + 4]);
+            fclose(fp);
+        }
+    }
     if (st.sync_error)  // qm1d_frame_grid: a grid barrier gave up; nothing of the frame is adopted
         return fail(SQ_E_HIP, "QM1D grid barrier timeout: a block of qm1d_frame_grid never arrived "
                               "(the frame is void, the state is the frame start)");

@@ -259,6 +259,9 @@ struct Qm1dArgs {
     int gbar;                   // qm1d_frame_grid: 1 = its own counter barrier (else cooperative groups)
     unsigned int bar_polls;     // ... the barrier's poll budget (0: kGridSpinMax)
     int bar_skip;               // ... (tests, SQ_QM1D_BAR_SKIP) this block never arrives at barrier 1; -1 none
+    unsigned long long *dbg;    // ... (diagnostics, SQ_QM1D_STAMPS) per block and step < 64, five 100 MHz clock
+                                //     stamps: step start, stores done, past the barrier, past the previous scan's
+                                //     outcome, scan done (nullable)
 };
 
 int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant: N > kQm1dRegMaxN)

@@ -710,10 +710,14 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     int stable = 1, steps = 0;
     const double *fin = A.f;
     double *fout = A.nf;
+    auto stamp = [&](int j, int ph) {  // diagnostics only (A.dbg, SQ_QM1D_STAMPS)
+        if (A.dbg != nullptr && t == 0 && j < 64) A.dbg[((size_t)b * 64 + j) * 5 + ph] = __builtin_amdgcn_s_memrealtime();
+    };
     for (int j = 0; j <= A.loops; ++j) {
         const int par = j & 1;
         double X[kGridK];
         double ix = -INFINITY, ia = -INFINITY;
+        stamp(j, 0);
         if (j < A.loops) {
             // 1. site updates of step j
             const unsigned long long step = A.tick + (unsigned long long)j;
@@ -781,6 +785,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                 bm[(2 * par + 1) * G + b] = ba;
             }
         }
+        stamp(j, 1);
         const unsigned int polls = A.bar_polls ? A.bar_polls : kGridSpinMax;
         if (A.gbar == 3) {
             if (!grid_barrier_flags(bar + 16, (unsigned int)(j + 1), &A.st->sync_error, polls,
@@ -798,6 +803,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             // here made every wave write back the L2 again each step
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
+        stamp(j, 2);
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
@@ -811,6 +817,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             }
         }
         if (j == A.loops) break;
+        stamp(j, 3);
         // 2b. step j's ordered scan
         double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
         totA = V;
@@ -847,6 +854,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         const unsigned long long tag1 = (unsigned long long)(j + 1);
         if (leader >= 0) atomicMax(lead, (tag1 << 32) | (unsigned long long)(leader + 1));
         if (un) atomicMax(unst, tag1);
+        stamp(j, 4);
         // omega's step j
         const unsigned long long step = A.tick + (unsigned long long)j;
         const f32x4n nwn = normals4(0ull, kStreamOmega, (uint32_t)step, (uint32_t)(step >> 32), A.k0, A.k1);
