@@ -708,30 +708,34 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     int E = A.st->lrgEl;
     double V = A.st->lrgVl, totA = 0.;
     int stable = 1, steps = 0;
-    const double *fin = A.f;
     double *fout = A.nf;
+    // The field of the previous step: this thread's own sites stay in
+    // registers; its two neighbour sites and f[mid] -- written by other
+    // threads and blocks -- are loaded right after each barrier, so the loads
+    // overlap the scan instead of opening the next step's site updates.
+    double fc[kGridK];
+#pragma unroll
+    for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? A.f[i0 + k] : 0.;
+    double fL = (own > 0 && i0 > 0) ? A.f[i0 - 1] : 0.;
+    double fR = (own > 0 && i0 + own < N) ? A.f[i0 + own] : 0.;
+    double fmid = A.f[mid];
     auto stamp = [&](int j, int ph) {  // diagnostics only (A.dbg, SQ_QM1D_STAMPS)
         if (A.dbg != nullptr && t == 0 && j < 64) A.dbg[((size_t)b * 64 + j) * 5 + ph] = __builtin_amdgcn_s_memrealtime();
     };
     for (int j = 0; j <= A.loops; ++j) {
         const int par = j & 1;
-        double X[kGridK];
+        double X[kGridK], vn[kGridK];
         double ix = -INFINITY, ia = -INFINITY;
         stamp(j, 0);
         if (j < A.loops) {
             // 1. site updates of step j
             const unsigned long long step = A.tick + (unsigned long long)j;
             const uint32_t slo = (uint32_t)step, shi = (uint32_t)(step >> 32);
-            const double Xm = fin[mid] + xcl((double)mid * a, om, pot);
+            const double Xm = fmid + xcl((double)mid * a, om, pot);
             const double den = (double)(A.runs + j + 1);
             double lmaxX = -INFINITY, lmaxA = -INFINITY;
             if (own > 0) {
                 f32x4n nq = normals4((unsigned long long)(i0 >> 2), kStreamField, slo, shi, A.k0, A.k1);
-                double fc[kGridK];
-#pragma unroll
-                for (int k = 0; k < kGridK; ++k) fc[k] = k < own ? fin[i0 + k] : 0.;
-                const double fL = i0 > 0 ? fin[i0 - 1] : 0.;
-                const double fR = i0 + own < N ? fin[i0 + own] : 0.;
 #pragma unroll
                 for (int k = 0; k < kGridK; ++k) {
                     if (k >= own) break;
@@ -764,12 +768,15 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     const double Xi = fi + xc;
                     nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
                     nx[k] = nx[k] + (Xi - nx[k]) / den;
+                    vn[k] = v;
                     fout[i] = v;
                     Xb[par][i] = X[k];
                 }
             }
-            ix = wave_incl_max(lmaxX, lane);
-            ia = wave_incl_max(lmaxA, lane);
+            // wave prefix maxima by DPP row scans (max is exact: the same values
+            // as any other order)
+            ix = dpp_incl_max(lmaxX);
+            ia = dpp_incl_max(lmaxA);
             if (lane == 63) {
                 s_wX[par][wv] = ix;
                 s_wA[par][wv] = ia;
@@ -804,6 +811,25 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         stamp(j, 2);
+        // every load the rest of the step needs that does not depend on the
+        // previous scan's outcome, issued together: the next step's neighbour
+        // sites and f[mid] (this step's output), and the block maxima (lane q:
+        // blocks q, q + 64, ...; exclusive prefix over the blocks before this
+        // one, and the total of |X'|)
+        double nL = 0., nR = 0., nmid = 0., pX = -INFINITY, pA = -INFINITY, tA = -INFINITY;
+        if (j < A.loops) {
+            nL = (own > 0 && i0 > 0) ? fout[i0 - 1] : 0.;
+            nR = (own > 0 && i0 + own < N) ? fout[i0 + own] : 0.;
+            nmid = fout[mid];
+            for (int q = lane; q < G; q += 64) {
+                const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
+                if (q < b) {
+                    pX = fmax(pX, qx);
+                    pA = fmax(pA, qa);
+                }
+                tA = fmax(tA, qa);
+            }
+        }
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
@@ -820,26 +846,15 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         stamp(j, 3);
         // 2b. step j's ordered scan
         double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
-        totA = V;
-        for (int q = 0; q < G; ++q) {
-            const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
-            if (q < b) {
-                runX = fmax(runX, qx);
-                runA = fmax(runA, qa);
-            }
-            totA = fmax(totA, qa);
-        }
+        runX = fmax(runX, dpp_all_max(pX));
+        runA = fmax(runA, dpp_all_max(pA));
+        totA = fmax(V, dpp_all_max(tA));
         for (int w = 0; w < wv; ++w) {
             runX = fmax(runX, s_wX[par][w]);
             runA = fmax(runA, s_wA[par][w]);
         }
-        double ex = __shfl_up(ix, 1, 64), ea = __shfl_up(ia, 1, 64);
-        if (lane == 0) {
-            ex = -INFINITY;
-            ea = -INFINITY;
-        }
-        runX = fmax(runX, ex);
-        runA = fmax(runA, ea);
+        runX = fmax(runX, dpp_from_left(ix, -INFINITY));  // lanes before this one (lane 0: none)
+        runA = fmax(runA, dpp_from_left(ia, -INFINITY));
         int un = 0, leader = -1;
 #pragma unroll
         for (int k = 0; k < kGridK; ++k) {
@@ -862,15 +877,20 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         if (nwo > (double)(N - 1) * a) om = 2 * (double)(N - 1) * a - nwo;
         else if (nwo < 0) om = -nwo;
         else om = nwo;
-        fin = fout;
+        // step j becomes the previous step
+#pragma unroll
+        for (int k = 0; k < kGridK; ++k) fc[k] = vn[k];
+        fL = nL;
+        fR = nR;
+        fmid = nmid;
         fout = (fout == A.nf) ? A.fs : A.nf;
     }
-    // unstable after step s: the break came before iteration s+1's swap, so
-    // fin is step s's output, as in the one-CU kernel (the host discards it)
+    // unstable after step s: the break came before iteration s+1's swap, so fc
+    // is step s's output, as in the one-CU kernel (the host discards it)
 #pragma unroll
     for (int k = 0; k < kGridK; ++k) {
         if (k >= own) break;
-        if (fin != A.nf) A.nf[i0 + k] = fin[i0 + k];
+        A.nf[i0 + k] = fc[k];
         A.nx[i0 + k] = nx[k];
         A.nxx0[i0 + k] = nxx0[k];
     }
