@@ -719,6 +719,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     double fL = (own > 0 && i0 > 0) ? A.f[i0 - 1] : 0.;
     double fR = (own > 0 && i0 + own < N) ? A.f[i0 + own] : 0.;
     double fmid = A.f[mid];
+    int myLead = -1;  // this thread's last leader in the previous step's scan (-1: none)
     auto stamp = [&](int j, int ph) {  // diagnostics only (A.dbg, SQ_QM1D_STAMPS)
         if (A.dbg != nullptr && t == 0 && j < 64) A.dbg[((size_t)b * 64 + j) * 5 + ph] = __builtin_amdgcn_s_memrealtime();
     };
@@ -769,8 +770,13 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     nxx0[k] = nxx0[k] + (Xi * Xm - nxx0[k]) / den;
                     nx[k] = nx[k] + (Xi - nx[k]) / den;
                     vn[k] = v;
-                    fout[i] = v;
-                    Xb[par][i] = X[k];
+                    // only what another thread reads: the thread's edge sites and
+                    // f[mid] (the next step's neighbours / running means), and X'
+                    // at the two sites the scan can need it at -- the current
+                    // leader E and this thread's last leader of the previous
+                    // scan (the new E is the largest such index, or E itself)
+                    if (k == 0 || k == own - 1 || i == mid) fout[i] = v;
+                    if (i == E || i == myLead) Xb[par][i] = X[k];
                 }
             }
             // wave prefix maxima by DPP row scans (max is exact: the same values
@@ -869,6 +875,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         const unsigned long long tag1 = (unsigned long long)(j + 1);
         if (leader >= 0) atomicMax(lead, (tag1 << 32) | (unsigned long long)(leader + 1));
         if (un) atomicMax(unst, tag1);
+        myLead = leader;
         stamp(j, 4);
         // omega's step j
         const unsigned long long step = A.tick + (unsigned long long)j;
