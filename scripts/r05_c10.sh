@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5, call 10: QM1D grid kernel storing only what other threads read --
+# Round 5, call 10/11: QM1D grid kernel, flag barrier with sc1 hand-offs (bar 4) --
 # bitwise tests, C1 sweep, stamps.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -9,12 +9,12 @@ T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
 timeout -k 10 120 $T tests/test_gpu_qm1d.py -k barrier_timeout > $O/barrier.log 2>&1 || { tail -30 $O/barrier.log; exit 2; }
 timeout -k 10 400 $T tests/test_gpu_qm1d.py tests/test_gpu_tauhost.py::test_config_c1_chain_through_tauhost > $O/qm1d.log 2>&1 || { tail -30 $O/qm1d.log; exit 3; }
 tail -2 $O/qm1d.log
-for r in 1 2; do for cfg in "3 4" "3 2" "1 4" "3 8"; do
+for r in 1 2; do for cfg in "4 4" "4 2" "3 4" "3 2"; do
   set -- $cfg
   SQ_QM1D_BAR=$1 SQ_QM1D_GK=$2 timeout -k 10 120 python3 scripts/bench_c1.py --frames 16 > $O/c1_bar$1_k$2_$r.log 2>&1 || { tail -5 $O/c1_bar$1_k$2_$r.log; exit 4; }
   echo "bar=$1 K=$2 run=$r $(grep '^{' $O/c1_bar$1_k$2_$r.log)"
 done; done
-for cfg in "3 4" "3 2"; do
+for cfg in "4 4" "4 2"; do
   set -- $cfg
   rm -f $O/stamps_bar$1_k$2.txt
   SQ_QM1D_BAR=$1 SQ_QM1D_GK=$2 SQ_QM1D_STAMPS=$O/stamps_bar$1_k$2.txt timeout -k 10 120 python3 scripts/bench_c1.py --frames 2 > $O/st.log 2>&1 || exit 5

@@ -643,6 +643,7 @@ __device__ __forceinline__ bool grid_barrier(unsigned int *ctr, unsigned int n, 
 // 8 / 4 / 2 = 16 / 32 / 64 blocks, profiles/r03/qm1d_grid/), and it polls with
 // acquire loads (an L1 invalidate per poll); flags cost one store per block.
 // Bounded like grid_barrier.
+template <bool FENCED = true>
 __device__ __forceinline__ bool grid_barrier_flags(unsigned int *flags, unsigned int n, int *err,
                                                    unsigned int polls, bool skip) {
     __shared__ int s_ok;
@@ -651,7 +652,7 @@ __device__ __forceinline__ bool grid_barrier_flags(unsigned int *flags, unsigned
     if (threadIdx.x < 64) {
         const int lane = (int)threadIdx.x, G = (int)gridDim.x;
         if (lane == 0 && !skip) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the block's writes, past the XCD's L2
+            if (FENCED) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the block's writes, past the XCD's L2
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __hip_atomic_store(flags + 16 * blockIdx.x, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -669,7 +670,7 @@ __device__ __forceinline__ bool grid_barrier_flags(unsigned int *flags, unsigned
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (ok) {
+        if (FENCED && ok) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // this CU's L1: the other blocks' writes
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -679,7 +680,26 @@ __device__ __forceinline__ bool grid_barrier_flags(unsigned int *flags, unsigned
     return s_ok != 0;
 }
 
-template <int kGridK>
+// SC1 (SQ_QM1D_BAR=4): the values one block hands to another -- edge sites,
+// f[mid], X' at the candidate leaders, the block maxima -- stored with sc1
+// stores (write-through) and read with sc1 loads (past the reader's L1), so
+// the flag barrier needs no release (L2 write-back) and no acquire (L1
+// invalidate): MI355X_MICROARCH.md's "Valid forms", one lane signalling for
+// its workgroup, 8-B sc1 stores and loads, hipMalloc memory.
+typedef __attribute__((address_space(1))) double gdouble;
+template <bool SC1>
+__device__ __forceinline__ double ld_x(const double *p) {
+    if constexpr (SC1)
+        return __hip_atomic_load((const gdouble *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool SC1>
+__device__ __forceinline__ void st_x(double *p, double v) {
+    if constexpr (SC1) __hip_atomic_store((gdouble *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+template <int kGridK, bool SC1>
 __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     cooperative_groups::grid_group grid = cooperative_groups::this_grid();
     unsigned int *bar = reinterpret_cast<unsigned int *>(A.ds + A.N) + 4;  // zeroed before the launch
@@ -693,9 +713,9 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     double *Xb[2] = {A.xs, A.ds};
     double *bm = A.xs + N;  // [parity][X | A][G]
     unsigned long long *lead = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lead + 1;
-    if (gt == 0) {
-        *lead = 0ull;
-        *unst = 0ull;
+    if (gt == 0) {  // write-through: the other blocks' atomics (and, SC1, loads) must see the zeros
+        __hip_atomic_store(lead, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(unst, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     double nx[kGridK], nxx0[kGridK], D[kGridK];
 #pragma unroll
@@ -775,8 +795,8 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     // at the two sites the scan can need it at -- the current
                     // leader E and this thread's last leader of the previous
                     // scan (the new E is the largest such index, or E itself)
-                    if (k == 0 || k == own - 1 || i == mid) fout[i] = v;
-                    if (i == E || i == myLead) Xb[par][i] = X[k];
+                    if (k == 0 || k == own - 1 || i == mid) st_x<SC1>(fout + i, v);
+                    if (i == E || i == myLead) st_x<SC1>(Xb[par] + i, X[k]);
                 }
             }
             // wave prefix maxima by DPP row scans (max is exact: the same values
@@ -794,15 +814,15 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
                     bx = fmax(bx, s_wX[par][w]);
                     ba = fmax(ba, s_wA[par][w]);
                 }
-                bm[(2 * par) * G + b] = bx;
-                bm[(2 * par + 1) * G + b] = ba;
+                st_x<SC1>(bm + (2 * par) * G + b, bx);
+                st_x<SC1>(bm + (2 * par + 1) * G + b, ba);
             }
         }
         stamp(j, 1);
         const unsigned int polls = A.bar_polls ? A.bar_polls : kGridSpinMax;
-        if (A.gbar == 3) {
-            if (!grid_barrier_flags(bar + 16, (unsigned int)(j + 1), &A.st->sync_error, polls,
-                                    j == 0 && b == A.bar_skip))
+        if (SC1 || A.gbar == 3) {
+            if (!grid_barrier_flags<!SC1>(bar + 16, (unsigned int)(j + 1), &A.st->sync_error, polls,
+                                          j == 0 && b == A.bar_skip))
                 return;  // a barrier gave up: the frame is void (the host reports it)
         } else {
             if (A.gbar) {
@@ -824,11 +844,11 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         // one, and the total of |X'|)
         double nL = 0., nR = 0., nmid = 0., pX = -INFINITY, pA = -INFINITY, tA = -INFINITY;
         if (j < A.loops) {
-            nL = (own > 0 && i0 > 0) ? fout[i0 - 1] : 0.;
-            nR = (own > 0 && i0 + own < N) ? fout[i0 + own] : 0.;
-            nmid = fout[mid];
+            nL = (own > 0 && i0 > 0) ? ld_x<SC1>(fout + i0 - 1) : 0.;
+            nR = (own > 0 && i0 + own < N) ? ld_x<SC1>(fout + i0 + own) : 0.;
+            nmid = ld_x<SC1>(fout + mid);
             for (int q = lane; q < G; q += 64) {
-                const double qx = bm[(2 * par) * G + q], qa = bm[(2 * par + 1) * G + q];
+                const double qx = ld_x<SC1>(bm + (2 * par) * G + q), qa = ld_x<SC1>(bm + (2 * par + 1) * G + q);
                 if (q < b) {
                     pX = fmax(pX, qx);
                     pA = fmax(pA, qa);
@@ -851,7 +871,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         if (j == A.loops) break;
         stamp(j, 3);
         // 2b. step j's ordered scan
-        double runX = (E >= 0 && E < N) ? Xb[par][E] : -INFINITY, runA = V;
+        double runX = (E >= 0 && E < N) ? ld_x<SC1>(Xb[par] + E) : -INFINITY, runA = V;
         runX = fmax(runX, dpp_all_max(pX));
         runA = fmax(runA, dpp_all_max(pA));
         totA = fmax(V, dpp_all_max(tA));
@@ -999,11 +1019,11 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
             if (e != hipSuccess) return e;
         }
         void *args[] = {&q};
-        const void *fn = kk == 2    ? (const void *)qm1d_frame_grid<2>
-                         : kk == 8  ? (const void *)qm1d_frame_grid<8>
-                         : kk == 16 ? (const void *)qm1d_frame_grid<16>
-                         : kk == 32 ? (const void *)qm1d_frame_grid<32>
-                                    : (const void *)qm1d_frame_grid<4>;
+        const bool sc1 = q.gbar == 4;
+#define SQ_GRIDK(K) (sc1 ? (const void *)qm1d_frame_grid<K, true> : (const void *)qm1d_frame_grid<K, false>)
+        const void *fn = kk == 2 ? SQ_GRIDK(2) : kk == 8 ? SQ_GRIDK(8) : kk == 16 ? SQ_GRIDK(16)
+                                                          : kk == 32 ? SQ_GRIDK(32) : SQ_GRIDK(4);
+#undef SQ_GRIDK
         if (q.gbar) {
             // the counter barrier needs every block resident, not the
             // cooperative-launch machinery (GWS, its own queue); a plain launch

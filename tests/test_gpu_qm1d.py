@@ -203,7 +203,7 @@ def test_large_chain_double_well_within_tolerance(gpu, oracle_mod):
         assert np.max(np.abs(d[k] - r[k])) <= tol
 
 
-@pytest.mark.parametrize("bar", ["3", "1", "0"])
+@pytest.mark.parametrize("bar", ["4", "3", "1", "0"])
 @pytest.mark.parametrize("N,pot,C,h", [(8192, 3, 1.0, 0.002), (32768, 0, 1.0, 0.01), (65536, 3, 1.0, 0.002),
                                        (4097, 0, 1.0, 0.002), (20000, 3, 1.0, 0.09)])
 def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
@@ -211,8 +211,9 @@ def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
     step) and the one-work-group frame (SQ_QM1D_GRID=0) are bit-identical with
     the noise on: field, running means, omega, the carried scan state and the
     verdict -- incl. a step size that makes the frame unstable part-way (last
-    case).  Every barrier form: per-block flags (SQ_QM1D_BAR=3), release /
-    acquire fences around one counter (1), cooperative groups (0)."""
+    case).  Every barrier form: per-block flags with sc1 hand-offs
+    (SQ_QM1D_BAR=4), per-block flags with release / acquire fences (3), one
+    counter with fences (1), cooperative groups (0)."""
     a, loops = 0.1, 40
     f, x, xx0 = _state(N, seed=11, amp=0.3)
     om = N * a / 2 + 0.013
@@ -230,7 +231,7 @@ def test_grid_frame_equals_one_cu_frame(gpu, monkeypatch, N, pot, C, h, bar):
     assert d1["omega"] == d0["omega"] and c1 == c0
 
 
-@pytest.mark.parametrize("bar", ["1", "3"])
+@pytest.mark.parametrize("bar", ["1", "3", "4"])
 def test_grid_barrier_timeout_returns_error(gpu, monkeypatch, bar):
     """The grid kernel's counter barrier is bounded: with a
     debug switch one block never arrives at the first barrier
@@ -281,7 +282,8 @@ def test_grid_sc1_handoff_c1_frames_bitwise(gpu, monkeypatch):
             st = [q.run_frame() for _ in range(2)]
             return st, q.download(), q.scan
     ref = run("0", "1")
-    for grid, bar, gk in (("1", "3", "8"), ("1", "1", "8"), ("1", "3", "2"), ("1", "3", "4")):
+    for grid, bar, gk in (("1", "3", "8"), ("1", "1", "8"), ("1", "3", "2"), ("1", "3", "4"), ("1", "4", "2"),
+                          ("1", "4", "4")):
         got = run(grid, bar, gk)
         assert got[0] == ref[0], (bar, got[0], ref[0])
         for k in ("f", "x", "xx0"):
