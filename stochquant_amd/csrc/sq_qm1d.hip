@@ -1000,7 +1000,8 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         // sites per thread: 8 (N = 32,768: 16 blocks, 11.8 ms per 1000-step
         // frame; 4: 14.2, 2: 22.6, 16: 18.6, 32: 51.3 -- profiles/r03/qm1d_grid/)
         const char *gk = getenv("SQ_QM1D_GK");
-        const int kk = gk ? atoi(gk) : 8;
+        int kk = gk ? atoi(gk) : 8;
+        if (kk != 1 && kk != 2 && kk != 4 && kk != 8 && kk != 16 && kk != 32) kk = 8;  // the instances built
         const int G = (a.N + kGridT * kk - 1) / (kGridT * kk);
         if (4 * G > kQm1dGridAux) return hipErrorInvalidValue;  // xs[N..]: the block maxima by parity
         Qm1dArgs q = a;
@@ -1021,8 +1022,8 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         void *args[] = {&q};
         const bool sc1 = q.gbar == 4;
 #define SQ_GRIDK(K) (sc1 ? (const void *)qm1d_frame_grid<K, true> : (const void *)qm1d_frame_grid<K, false>)
-        const void *fn = kk == 2 ? SQ_GRIDK(2) : kk == 8 ? SQ_GRIDK(8) : kk == 16 ? SQ_GRIDK(16)
-                                                          : kk == 32 ? SQ_GRIDK(32) : SQ_GRIDK(4);
+        const void *fn = kk == 1 ? SQ_GRIDK(1) : kk == 2 ? SQ_GRIDK(2) : kk == 8 ? SQ_GRIDK(8)
+                         : kk == 16 ? SQ_GRIDK(16) : kk == 32 ? SQ_GRIDK(32) : SQ_GRIDK(4);
 #undef SQ_GRIDK
         if (q.gbar) {
             // the counter barrier needs every block resident, not the
