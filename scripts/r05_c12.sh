@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 O=gpurun_out/${1:-r05_c12}
 mkdir -p $O
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
-SQ_QM1D_GK=1 SQ_QM1D_BAR=4 timeout -k 10 300 $T tests/test_gpu_qm1d.py -k "grid_frame_equals or large_chain" > $O/qm1d_k1.log 2>&1 || { tail -30 $O/qm1d_k1.log; exit 3; }
+timeout -k 10 300 $T tests/test_gpu_qm1d.py -k "c1_frames" > $O/qm1d_k1.log 2>&1 || { tail -30 $O/qm1d_k1.log; exit 3; }
 tail -1 $O/qm1d_k1.log
 for r in 1 2 3; do for cfg in "4 1" "4 2" "1 8"; do
   set -- $cfg

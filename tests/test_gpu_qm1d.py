@@ -283,7 +283,7 @@ def test_grid_sc1_handoff_c1_frames_bitwise(gpu, monkeypatch):
             return st, q.download(), q.scan
     ref = run("0", "1")
     for grid, bar, gk in (("1", "3", "8"), ("1", "1", "8"), ("1", "3", "2"), ("1", "3", "4"), ("1", "4", "2"),
-                          ("1", "4", "4")):
+                          ("1", "4", "4"), ("1", "4", "1")):
         got = run(grid, bar, gk)
         assert got[0] == ref[0], (bar, got[0], ref[0])
         for k in ("f", "x", "xx0"):
