@@ -997,18 +997,23 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
     const char *ge = getenv("SQ_QM1D_GRID");  // read per frame (tests switch it within a process)
     const bool grid = ge ? atoi(ge) != 0 : true;
     if (grid && a.N <= kQm1dMaxN) {
-        // sites per thread: 8 (N = 32,768: 16 blocks, 11.8 ms per 1000-step
-        // frame; 4: 14.2, 2: 22.6, 16: 18.6, 32: 51.3 -- profiles/r03/qm1d_grid/)
         const char *gk = getenv("SQ_QM1D_GK");
-        int kk = gk ? atoi(gk) : 8;
+        // sites per thread: the fewest that keep G <= 128 blocks (N = 32,768: 1 site,
+        // 128 blocks, 4.92 ms per 1000-step frame; 2 sites 5.03; 4 sites 5.77; 8
+        // sites 8.0 -- profiles/r05/c11, c12); SQ_QM1D_GK pins it
+        int kk = 1;
+        while (kk < 32 && (a.N + kGridT * kk - 1) / (kGridT * kk) > 128) kk *= 2;
+        if (gk) kk = atoi(gk);
         if (kk != 1 && kk != 2 && kk != 4 && kk != 8 && kk != 16 && kk != 32) kk = 8;  // the instances built
         const int G = (a.N + kGridT * kk - 1) / (kGridT * kk);
         if (4 * G > kQm1dGridAux) return hipErrorInvalidValue;  // xs[N..]: the block maxima by parity
         Qm1dArgs q = a;
-        // the counter barrier: N = 32,768 10.8 vs 11.7 ms per 1000-step frame with
-        // cooperative groups' grid.sync (profiles/r03/qm1d_grid/); SQ_QM1D_BAR=0
+        // the barrier (SQ_QM1D_BAR): 4 (default) per-block flags with sc1 hand-offs
+        // and no fences; 3 per-block flags with release / acquire fences; 1 one
+        // counter with fences (round 3's, 10.8 ms per C1 frame vs 11.7 with 0,
+        // cooperative groups' grid.sync: profiles/r03/qm1d_grid/)
         const char *gb = getenv("SQ_QM1D_BAR");
-        q.gbar = gb ? atoi(gb) : 1;
+        q.gbar = gb ? atoi(gb) : 4;
         // tests: a block that never arrives (SQ_QM1D_BAR_SKIP=b) and a shorter poll budget
         const char *bs = getenv("SQ_QM1D_BAR_SKIP"), *bp = getenv("SQ_QM1D_BAR_POLLS");
         q.bar_skip = bs ? atoi(bs) : -1;
@@ -1028,7 +1033,7 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         if (q.gbar) {
             // the counter barrier needs every block resident, not the
             // cooperative-launch machinery (GWS, its own queue); a plain launch
-            // of G <= the chip's resident capacity (G = 16 at N = 32,768) keeps
+            // of G <= the chip's resident capacity (G = 128 at N = 32,768) keeps
             // the frame on the context's stream like every other kernel, and
             // profilers that mishandle cooperative dispatches at exit see none
             int dev = 0, cus = 0, per_cu = 0;
