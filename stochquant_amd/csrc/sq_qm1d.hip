@@ -573,13 +573,15 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
 
 // The same frame for N > 4096 on the whole chip (config C1's 32,768-site
 // chain; qm1d_frame_kernel_glob runs it on one CU): G = ceil(N / (256 K))
-// cooperative blocks of 256 threads, thread g owning sites [Kg, Kg+K) in
-// registers (drift checks and running means never leave them; K = 8).  ONE grid
+// co-resident blocks of 256 threads, thread g owning sites [Kg, Kg+K) in
+// registers -- the field, the drift checks and the running means never leave
+// them (K = the fewest sites with G <= 128: 1 at N = 32,768).  ONE grid
 // barrier per step, between
-//   1. site updates from the old field (neighbours and f[mid] read from
-//      global memory, written by their owners before the last barrier),
-//      running means, guard, X' (parked in a by-parity buffer), drift check,
-//      per-block maxima of X' and |X'| (by parity);
+//   1. site updates from the old field (the two neighbour sites and f[mid]
+//      loaded right after the previous barrier, written by their owners
+//      before it), running means, guard, X', drift check; stored for other
+//      threads only: the thread's edge sites, f[mid], X' at the sites the
+//      next scan can need (by parity), the per-block maxima of X' and |X'|;
 //   2. the outcome of the previous step's scan (its leader and instability:
 //      step-tagged atomic-max words its scan wrote before this barrier, so no
 //      slot needs resetting) -- an unstable previous step ends the frame here,
@@ -596,7 +598,8 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
 // expressions, the same order of every max; tests/test_gpu_qm1d.py::
 // test_grid_frame_equals_one_cu_frame, and the oracle tests at N > 4096).
 // Scratch: xs / ds (N + kGridAux doubles each) hold X' of even / odd steps,
-// xs[N..] the block maxima, ds[N..] the two tagged words.
+// xs[N..] the block maxima, ds[N..] the two tagged words, the counter and the
+// per-block flags of the barrier.
 constexpr int kGridT = 256;
 
 // Grid barrier of a grid whose blocks are all co-resident: thread 0 of
