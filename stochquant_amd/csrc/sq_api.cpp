@@ -2720,6 +2720,12 @@ int sq_set_noise(sq_ctx *c, double C) {
     if (!c) return fail(SQ_E_ARG, "null context");
     // the PHI4 guard fast path bounds |sigma xi| by 16 sqrt(2 dtau) |C| (create_phi4), dtau <= 1e20
     if (!std::isfinite(C) || std::fabs(C) > 1e12) return fail(SQ_E_ARG, "C must be finite, |C| <= 1e12");
+    if (is_phi4(c)) {  // create_phi4's bound with the new C at the current dtau
+        const double cl = c->p.clamp, h = c->dtau;
+        const double drift = 12.0 * cl + std::fabs(c->p.m2) * cl + std::fabs(c->p.lambda) / 6.0 * cl * cl * cl;
+        if (!(h * drift + cl + 16.0 * sqrt(2.0 * h) * std::fabs(C) < 1e30))
+            return fail(SQ_E_ARG, "C too large for the guard's fast path at this dtau (dtau * drift + noise >= 1e30)");
+    }
     c->p.C = C;
     return SQ_OK;
 }
