@@ -276,7 +276,9 @@ int sq_phi4_launch_info(sq_ctx *ctx, char *name, size_t cap, long long *grid_thr
 const char *sq_build_id(void);
 /* Noise amplitude C (argv[6], sigma = C sqrt(2 Δτ), tau_kernel.cl:112) of an
  * open context; C = 0 runs the deterministic drift-only update (bench.py's
- * oracle_check).  Not collective: every rank sets the same C. */
+ * oracle_check).  Not collective: every rank sets the same C.  SQ_E_ARG for
+ * |C| > 1e12, and (PHI4) when the new C breaks the creation-time bound of the
+ * guard's fast path at the current Δτ. */
 int sq_set_noise(sq_ctx *ctx, double C);
 /* PHI4, one slab without an exchange, fused launches: run the next two steps
  * (one fused launch, as sq_step(ctx, 2)) with per-block stamps of the
