@@ -256,6 +256,10 @@ struct sq_ctx {
     unsigned int *gate_word = nullptr;  // fine-grained: stream B writes ++gate_seq behind each exchange
     unsigned int gate_seq = 0;
     int *gate_err = nullptr;
+    // sticky: a gated rim chunk timed out, so the field's rim planes are stale;
+    // every call that would use the field fails until a new field is uploaded
+    // or initialised (gate_check / gate_reset)
+    bool gate_failed = false;
     struct {
         bool on;
         int tlo0, thi0, tlen;
@@ -939,6 +943,29 @@ int phi4_block(sq_ctx *c, int g) {
 
 int phi4_join(sq_ctx *c);
 
+// Gated rim chunks that gave up waiting for their exchange (tb_gate_wait) store
+// nothing, so the field is corrupt from then on: the error is sticky on the
+// context.  read_device: the caller has joined the streams, read the device
+// word (otherwise only the sticky flag, no synchronisation).
+int gate_check(sq_ctx *c, bool read_device) {
+    if (!c->gate_failed && read_device && c->gate_err) {
+        int e = 0;
+        SQ_HIP(hipMemcpy(&e, c->gate_err, sizeof e, hipMemcpyDeviceToHost));
+        if (e) c->gate_failed = true;
+    }
+    if (c->gate_failed)
+        return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange (their chunks "
+                               "were not stored; the field is corrupt until it is uploaded or initialised again)");
+    return SQ_OK;
+}
+
+// a new field replaces every plane: the timed-out chunks no longer matter
+int gate_reset(sq_ctx *c) {
+    if (c->gate_err) SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
+    c->gate_failed = false;
+    return SQ_OK;
+}
+
 // Ghost depth by measurement (slab paths): G in {4, 8, 16} (<= the allocated
 // depth), each timed over two blocks after one warm-up block on the interior
 // stream; across ranks the per-candidate times are max-reduced (RCCL or peer
@@ -1580,7 +1607,13 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     // diagnostics (SQ_QM1D_STAMPS=<path>, grid kernel): per-block phase stamps of
     // the frame's first 64 steps, appended to <path> as text (block step t0..t4)
     const char *dpath = getenv("SQ_QM1D_STAMPS");
-    const size_t ndbg = (size_t)sq::kQm1dMaxN / 512 * 64 * 5;  // up to 128 blocks
+    const size_t ndbg = (size_t)sq::kQm1dStampBlocks * 64 * 5;  // the kernel stamps no block past these
+    struct DbgFree {  // every return path below frees the stamp buffer
+        unsigned long long *&p;
+        ~DbgFree() {
+            if (p) (void)hipFree(p);
+        }
+    } dbg_free{a.dbg};
     if (dpath && c->N > sq::kQm1dRegMaxN) {
         SQ_HIP(hipMalloc(&a.dbg, ndbg * sizeof(unsigned long long)));
         SQ_HIP(hipMemsetAsync(a.dbg, 0, ndbg * sizeof(unsigned long long), c->qstream));
@@ -1596,7 +1629,6 @@ int qm1d_frame(sq_ctx *c, int *stable) {
     if (a.dbg) {
         std::vector<unsigned long long> h(ndbg);
         SQ_HIP(hipMemcpy(h.data(), a.dbg, ndbg * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        (void)hipFree(a.dbg);
         if (FILE *fp = fopen(dpath, "a")) {
             for (size_t q = 0; q < ndbg / 5; ++q)
                 if (h[5 * q])
@@ -1743,6 +1775,8 @@ int phi4_frame(sq_ctx *c, int *stable) {
     SQ_HIP(hipMemsetAsync(c->frame_cur, 0, c->frame_bytes, s0.sA));
     c->frame_rec_zero = true;
     SQ_HIP(hipStreamSynchronize(s0.sA));
+    rc = gate_check(c, true);  // a timed-out rim chunk: no verdict from a corrupt field
+    if (rc) return rc;
     const char *hb = static_cast<const char *>(c->frame_host);
     const unsigned long long *md = reinterpret_cast<const unsigned long long *>(hb);
     const unsigned int *am = reinterpret_cast<const unsigned int *>(hb + nrec * sizeof(unsigned long long));
@@ -2258,7 +2292,8 @@ int sq_run_frame(sq_ctx *c, int *stable) {
     // one frame: the host-decided path (one read-back, 454 vs 478 us per 256^3
     // 20-step frame for the device controller's state upload and read-back);
     // sq_run_frames keeps the decisions on the device across frames
-    int rc = is_phi4(c) ? phi4_frame(c, stable) : qm1d_frame(c, stable);
+    int rc = is_phi4(c) ? gate_check(c, false) : SQ_OK;
+    if (!rc) rc = is_phi4(c) ? phi4_frame(c, stable) : qm1d_frame(c, stable);
     if (rc) return rc;
     adapt(c, *stable);
     c->perf.frame_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -2271,7 +2306,8 @@ int sq_run_frames(sq_ctx *c, int nframes, int *stable, double *dtau) {
     DeviceGuard g(c->dev);
     const auto t0 = std::chrono::steady_clock::now();
     if (is_phi4(c)) {
-        int rc = phi4_frames_dev(c, nframes, stable, dtau);
+        int rc = gate_check(c, false);
+        if (!rc) rc = phi4_frames_dev(c, nframes, stable, dtau);
         if (rc) return rc;
     } else {
         for (int f = 0; f < nframes; ++f) {
@@ -2290,6 +2326,10 @@ int sq_step(sq_ctx *c, int nsteps) {
     if (!is_phi4(c)) return fail(SQ_E_STATE, "sq_step is for PHI4 contexts (QM1D uses sq_run_frame)");
     if (nsteps < 0) return fail(SQ_E_ARG, "nsteps < 0");
     DeviceGuard g(c->dev);
+    {
+        int rc = gate_check(c, false);  // a known timeout: no more steps on the corrupt field
+        if (rc) return rc;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     EvPair *region = nullptr;
     if (c->profiling == 2 && nsteps > 0) {
@@ -2300,6 +2340,10 @@ int sq_step(sq_ctx *c, int nsteps) {
     {
         int rc = phi4_steps(c, nsteps);
         if (rc) return rc;
+    }
+    if (c->gate_err) {  // tests: SQ_DIAG_GATE_ERR=1 flags a gate timeout as tb_gate_wait would
+        const char *ge = getenv("SQ_DIAG_GATE_ERR");
+        if (ge && atoi(ge) != 0) SQ_HIP(hipMemsetAsync(c->gate_err, 1, 1, c->slabs[0].sA));
     }
     if (region) {
         SQ_HIP(hipEventRecord(region->b, c->slabs[0].sA));
@@ -2355,16 +2399,7 @@ int sq_sync(sq_ctx *c) {
     if (c->qstream) SQ_HIP(hipStreamSynchronize(c->qstream));
     int rc = phi4_join(c);
     if (rc) return rc;
-    if (c->gate_err) {  // a gated rim chunk gave up waiting for its exchange (tb_gate_wait)
-        int e = 0;
-        SQ_HIP(hipMemcpy(&e, c->gate_err, sizeof e, hipMemcpyDeviceToHost));
-        if (e) {  // reported once: cleared, so later calls see only new timeouts
-            SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
-            return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange (their "
-                                   "chunks were not stored)");
-        }
-    }
-    return SQ_OK;
+    return gate_check(c, true);  // a gated rim chunk gave up waiting for its exchange: sticky
 }
 
 int sq_slab(sq_ctx *c, long long *nz_local, long long *z0) {
@@ -2510,6 +2545,10 @@ int sq_upload_field(sq_ctx *c, const float *phi, size_t count) {
     for (auto &s : c->slabs) need += (size_t)s.nz * plane;
     if (count != need) return fail(SQ_E_ARG, "field size mismatch");
     SQ_HIP(hipDeviceSynchronize());
+    {
+        int rc = gate_reset(c);
+        if (rc) return rc;
+    }
     size_t off = 0;
     for (auto &s : c->slabs) {
         SQ_HIP(hipMemcpy(plane0(c, s, c->cur), phi + off, (size_t)s.nz * plane * sizeof(float),
@@ -2530,6 +2569,7 @@ int sq_download_field(sq_ctx *c, float *phi, size_t count) {
     for (auto &s : c->slabs) need += (size_t)s.nz * plane;
     if (count != need) return fail(SQ_E_ARG, "field size mismatch");
     int rc = phi4_join(c);
+    if (!rc) rc = gate_check(c, true);
     if (rc) return rc;
     size_t off = 0;
     for (auto &s : c->slabs) {
@@ -2545,6 +2585,7 @@ int sq_init_field(sq_ctx *c, float amp) {
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
     DeviceGuard g(c->dev);
     int rc = phi4_join(c);
+    if (!rc) rc = gate_reset(c);
     if (rc) return rc;
     for (auto &s : c->slabs)
         SQ_HIP(sq::phi4_init_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, (uint32_t)c->p.seed,
@@ -2560,6 +2601,7 @@ int sq_init_field_hash(sq_ctx *c, double amp, unsigned long long key) {
     if (!std::isfinite(amp) || std::fabs(amp) > 1e30) return fail(SQ_E_ARG, "amp must be finite");
     DeviceGuard g(c->dev);
     int rc = phi4_join(c);
+    if (!rc) rc = gate_reset(c);
     if (rc) return rc;
     for (auto &s : c->slabs)
         SQ_HIP(sq::phi4_init_hash_launch(plane0(c, s, c->cur), c->Lx, c->Ly, s.nz, s.z0, key, amp, s.sA));

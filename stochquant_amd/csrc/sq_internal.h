@@ -268,6 +268,9 @@ int qm1d_sites_per_thread(int N);  // 0 if N unsupported (global-memory variant:
 constexpr int kQm1dMaxN = 1024 * 64;
 constexpr int kQm1dRegMaxN = 4096;  // register-resident frame kernel up to here; beyond, f ping-pong + scan scratch
 constexpr int kQm1dGridAux = 2048;
+// SQ_QM1D_STAMPS diagnostics: the stamp buffer's blocks (the grid kernel's default G
+// is at most this; SQ_QM1D_GK can force more); blocks past it record nothing
+constexpr int kQm1dStampBlocks = kQm1dMaxN / 512;
 // device bytes the precomputed frame tables may take (loops x N x 4-16 B); a
 // frame longer than this at its N is refused rather than allocated
 constexpr size_t kQm1dTableCap = size_t(16) << 30;  // N > kQm1dRegMaxN: xs and ds hold N + this many doubles (qm1d_frame_grid)

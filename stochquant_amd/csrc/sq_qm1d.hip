@@ -598,8 +598,8 @@ __global__ __launch_bounds__(kMaxThreads) void qm1d_frame_kernel_glob(const Qm1d
 // expressions, the same order of every max; tests/test_gpu_qm1d.py::
 // test_grid_frame_equals_one_cu_frame, and the oracle tests at N > 4096).
 // Scratch: xs / ds (N + kGridAux doubles each) hold X' of even / odd steps,
-// xs[N..] the block maxima, ds[N..] the two tagged words, the counter and the
-// per-block flags of the barrier.
+// xs[N..] the block maxima, ds[N..] the tagged words (leader by parity,
+// instability), the counter and the per-block flags of the barrier.
 constexpr int kGridT = 256;
 
 // Grid barrier of a grid whose blocks are all co-resident: thread 0 of
@@ -715,9 +715,17 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     const double h = A.h, a = A.a, a2 = A.a2;
     double *Xb[2] = {A.xs, A.ds};
     double *bm = A.xs + N;  // [parity][X | A][G]
-    unsigned long long *lead = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lead + 1;
+    // The leader word comes in two copies by step parity: scan j writes tag j+1
+    // into lead[(j+1)&1] and step j+1 reads it back; the next write to that copy
+    // is scan j+2's, behind barrier j+3, which no block passes before every
+    // block has read it.  (One shared word let a block that left barrier j+2
+    // early overwrite tag j+1 with j+2 before a slower block had read it.)  The
+    // copies: ds[N] bytes 0 and 24 (the barrier counter sits at byte 16).
+    unsigned long long *lw = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lw + 1;
+    unsigned long long *lead[2] = {lw, lw + 3};
     if (gt == 0) {  // write-through: the other blocks' atomics (and, SC1, loads) must see the zeros
-        __hip_atomic_store(lead, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lead[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lead[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(unst, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     double nx[kGridK], nxx0[kGridK], D[kGridK];
@@ -744,7 +752,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     double fmid = A.f[mid];
     int myLead = -1;  // this thread's last leader in the previous step's scan (-1: none)
     auto stamp = [&](int j, int ph) {  // diagnostics only (A.dbg, SQ_QM1D_STAMPS)
-        if (A.dbg != nullptr && t == 0 && j < 64) A.dbg[((size_t)b * 64 + j) * 5 + ph] = __builtin_amdgcn_s_memrealtime();
+        if (A.dbg != nullptr && t == 0 && j < 64 && b < kQm1dStampBlocks) A.dbg[((size_t)b * 64 + j) * 5 + ph] = __builtin_amdgcn_s_memrealtime();
     };
     for (int j = 0; j <= A.loops; ++j) {
         const int par = j & 1;
@@ -862,7 +870,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
-            const unsigned long long lv = __hip_atomic_load(lead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long lv = __hip_atomic_load(lead[j & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((lv >> 32) == tag) E = (int)(lv & 0xffffffffull) - 1;
             V = totA;
             steps = j;
@@ -896,7 +904,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             runA = fmax(runA, absol(X[k]));
         }
         const unsigned long long tag1 = (unsigned long long)(j + 1);
-        if (leader >= 0) atomicMax(lead, (tag1 << 32) | (unsigned long long)(leader + 1));
+        if (leader >= 0) atomicMax(lead[(j + 1) & 1], (tag1 << 32) | (unsigned long long)(leader + 1));
         if (un) atomicMax(unst, tag1);
         myLead = leader;
         stamp(j, 4);
@@ -1021,7 +1029,7 @@ hipError_t qm1d_frame_launch(const Qm1dArgs &a, hipStream_t s) {
         const char *bs = getenv("SQ_QM1D_BAR_SKIP"), *bp = getenv("SQ_QM1D_BAR_POLLS");
         q.bar_skip = bs ? atoi(bs) : -1;
         q.bar_polls = bp ? (unsigned int)strtoul(bp, nullptr, 10) : 0u;
-        if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (after the tagged words); the
+        if (q.gbar) {  // the counter barrier's word: ds[N] + 16 bytes (between the tagged words); the
                        // flag barrier's G words 64 B apart after it (ds[N] + 80 bytes: < kQm1dGridAux doubles)
             if (80 + 64 * (size_t)G > sizeof(double) * kQm1dGridAux) return hipErrorInvalidValue;
             hipError_t e = hipMemsetAsync(reinterpret_cast<unsigned int *>(q.ds + q.N) + 4, 0, 64 + 64 * (size_t)G, s);

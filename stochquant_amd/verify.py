@@ -89,14 +89,20 @@ def load_oracle_golden(path=ORACLE_GOLDEN):
         return {}
 
 
-def run_oracle_protocol(lat, corrupt=False):
-    """The noise-off parity protocol (collective in multi-rank contexts): C = 0,
-    this rank's slab of hash_field (sq_init_field_hash, on the device), the step counter at 0,
-    CHECK_STEPS steps; returns the slab digest.  With the noise off the step is
+def run_oracle_protocol(lat, corrupt=False, noise=False):
+    """The parity protocol (collective in multi-rank contexts): C = 0 (noise
+    False) or C = 1 (noise True), this rank's slab of hash_field
+    (sq_init_field_hash, on the device), the step counter at 0, CHECK_STEPS
+    steps; returns the slab digest.  With the noise off the step is
     deterministic fp32 arithmetic, so the digest must equal the oracle's
-    (oracle/orc_phi4.c, tests/golden/make_oracle_slabs.py) bit for bit."""
+    (oracle/orc_phi4.c, tests/golden/make_oracle_slabs.py) bit for bit.  With
+    it on the field is finite and inside the clamp, so the steps run the
+    timed instance (the noise path with the guard's fast path) and the digest
+    must equal the oracle's in device-transcendental mode: the same Philox
+    words, each Box-Muller factor the device's (sq_selftest_bm_tables) --
+    oracle_check_noise also compares those tables' digest."""
     C0 = float(lat.params.C)
-    lat.set_noise(0.0)
+    lat.set_noise(1.0 if noise else 0.0)
     try:
         lat.init_field_hash(HASH_FIELD_AMP, HASH_FIELD_KEY)   # = hash_field, generated on the device
         lat.step_counter = 0
@@ -109,14 +115,46 @@ def run_oracle_protocol(lat, corrupt=False):
         lat.set_noise(C0)
 
 
-def oracle_check(digests, shape, nranks, golden=None):
-    """'pass' / 'fail' / 'no golden' of the noise-off digests against the oracle's."""
-    g = (load_oracle_golden() if golden is None else golden).get(golden_key(shape, nranks))
+def oracle_check(digests, shape, nranks, golden=None, noise=False):
+    """'pass' / 'fail' / 'no golden' of the protocol's digests against the oracle's."""
+    key = golden_key(shape, nranks)
+    g = (load_oracle_golden() if golden is None else golden).get(NOISE_PREFIX + key if noise else key)
     if g is None:
         return "no golden"
     if len(digests) != nranks or len(g["slabs"]) != nranks:
         return "fail"
     return "pass" if all(d == e for d, e in zip(digests, g["slabs"])) else "fail"
+
+
+NOISE_PREFIX = "noise:"      # oracle_slabs.json keys of the C = 1 digests
+BM_TABLES_KEY = "bm_tables"  # ... and the digest of the device tables they were made with
+
+
+def bm_tables(device=0):
+    """The device's Box-Muller factors (sq_selftest_bm_tables): 4 x 2^23 float32."""
+    import ctypes
+    from . import _lib
+    t = np.empty(4 << 23, np.float32)
+    _lib.call("sq_selftest_bm_tables", int(device), t.ctypes.data_as(ctypes.POINTER(ctypes.c_float)))
+    return t
+
+
+def bm_tables_digest(tables):
+    return hashlib.blake2b(np.ascontiguousarray(tables, dtype=np.float32).tobytes(), digest_size=16).hexdigest()
+
+
+def oracle_check_noise(digests, table_digests, shape, nranks, golden=None):
+    """The C = 1 protocol's verdict: 'no golden' without committed digests for
+    this lattice, 'tables differ' when any rank's device tables are not the
+    ones the oracle digests were made with (no comparison then), else 'pass' /
+    'fail'."""
+    g = load_oracle_golden() if golden is None else golden
+    want = g.get(BM_TABLES_KEY, {}).get("blake2b")
+    if g.get(NOISE_PREFIX + golden_key(shape, nranks)) is None or want is None:
+        return "no golden"
+    if any(t != want for t in table_digests):
+        return "tables differ"
+    return oracle_check(digests, shape, nranks, golden=g, noise=True)
 
 
 def run_protocol(lat, corrupt=False):

@@ -84,3 +84,18 @@ def gpu(sqlib):
     if n < 1:
         pytest.fail("no HIP device visible: gpu tests must run on the MI355X box")
     return 0
+
+
+# fp32 tolerance of a noise-on phi^4 step against the MATHEMATICAL oracle (its
+# normals evaluated in double): per step |d| <= PHI4_STEP_ATOL + PHI4_STEP_RTOL
+# |phi'|, k steps k x (the update is a contraction for the tested parameters).
+# Constants: see tests/test_gpu_phi4.py's header and DESIGN.md §3.
+def tol_report(name, err, steps, ref, rtol):
+    """Print the measured maximum of a within-tolerance check and the per-step
+    absolute term it needs beside `rtol` (grep 'TOL ' in a -s run), and return
+    that term."""
+    import numpy as np
+    err = np.asarray(err, dtype=np.float64)
+    need = float(np.max((err - steps * rtol * np.abs(np.asarray(ref, dtype=np.float64))) / steps))
+    print(f"TOL {name} max_err={float(err.max()):.4e} steps={steps} atol_needed={need:.4e}", flush=True)
+    return need

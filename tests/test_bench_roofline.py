@@ -42,10 +42,10 @@ class _Lat:
 PERF = {"steps": 20, "kernel_launches": 10, "fused_steps": 20, "step_kernel_launches": 20, "step_kernel_ms": 0.33}
 
 
-def _profile(tmp_path, build, kernel=HOT, grid=327680):
+def _profile(tmp_path, build, kernel=HOT, grid=327680, rocprof_us=32.2):
     rec = {"kernel": f"void sq::(anonymous namespace)::{kernel}(sq::Phi4StepArgs)", "grid": grid,
            "build_id_phi4": build, "valu_busy_cycles_per_launch": 59187200.0, "hbm_bytes_per_launch": 151132160.0,
-           "rocprof_avg_us": 32.2}
+           "rocprof_avg_us": rocprof_us, "rocprof_median_us": rocprof_us}
     p = tmp_path / "driver_profile.json"
     p.write_text(json.dumps({"command": "python3 bench.py --steps 20 --warmup 5", "configs": {"256": rec}}))
     return str(p)
@@ -107,3 +107,18 @@ def test_committed_profile_describes_this_build(build):
         pytest.skip("no profile committed for this round yet")
     rec = json.load(open(path))["configs"]["256"]
     assert rec.get("build_id_phi4") and bench.short_kernel(rec["kernel"]) == HOT
+
+
+@pytest.mark.parametrize("rocprof_us,mismatch", [(32.2, False), (33.9, False), (35.0, True), (30.0, True)])
+def test_profile_timing_mismatch_is_flagged(monkeypatch, tmp_path, build, rocprof_us, mismatch):
+    """a record whose rocprof launch time is more than 3 %
+    off this run's live launch (33.0 us here) is flagged and its durations are
+    not quoted; the clock-independent counts still divide the live time."""
+    rl = _roofline(monkeypatch, tmp_path, _Lat(), _profile(tmp_path, build["phi4"], rocprof_us=rocprof_us))
+    assert rl["profile_timing_mismatch"] is mismatch
+    assert rl["launch_us_vs_rocprof_avg"] == round(33.0 / rocprof_us, 4)
+    assert ("profile_rocprof_avg_us" in rl) is (not mismatch)
+    assert ("profile_rocprof_median_us" in rl) is (not mismatch)
+    # frac_hbm_real and the VALU fraction come from the live launch time either way
+    assert rl["frac_hbm_real"] == round(151132160.0 / 33e-6 / 1e9 / 8000.0, 4)
+    assert rl["frac"] == round(59187200.0 / 33e-6 / 1e9 / (1024 * 2.4), 4)

@@ -13,6 +13,8 @@ import pytest
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
+from conftest import tol_report
+
 pytestmark = pytest.mark.gpu
 
 STEP_ATOL = 4e-6
@@ -41,6 +43,7 @@ def test_phi4_random_shapes(gpu, oracle_mod, Lx, Ly, Lz, steps, C, seed, dtau):
         assert np.array_equal(got, ref)
     else:
         err = np.abs(got.astype(np.float64) - ref)
+        tol_report(f"fuzz{shape},dtau={dtau}", err, steps, ref, STEP_RTOL)
         assert np.all(err <= steps * (STEP_ATOL + STEP_RTOL * np.abs(ref)))
 
 

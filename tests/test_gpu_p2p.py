@@ -136,6 +136,10 @@ def test_p2p_unconnected_context_refuses_to_step(gpu):
     (3, (256, 16, 96), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2"}),  # core pairs ahead of the exchange
     (3, (256, 16, 96), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2", "SQ_RIMS_B": "1"}),  # rims on stream B
     (2, (256, 16, 64), 30, {"SQ_GHOST": "16", "SQ_CORE_PAIRS": "0"}),  # no core/rim split
+    # the driver's N = 8 shape: eight rank processes, each
+    # slab's two peers distinct ranks, fused pairs and core pairs
+    (8, (64, 8, 64), 17, {"SQ_GHOST": "4"}),
+    (8, (256, 16, 256), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2"}),
 ])
 def test_p2p_ranks_bitwise_vs_single_slab(gpu, nranks, shape, steps, env):
     phi0 = _field0(shape)

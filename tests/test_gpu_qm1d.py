@@ -66,7 +66,8 @@ def test_frame_within_tolerance(gpu, oracle_mod, N, pot, C):
     tol = loops * (sig * 1.4e-5 + 2e-6)
     for k in ("f", "x", "xx0"):
         err = np.max(np.abs(d[k] - r[k]))
-        print(k, err, tol)
+        print(f"TOL qm1d_frame N={N} pot={pot} C={C} {k} max_err={err:.4e} sig={sig:.4e} loops={loops} tol={tol:.4e}",
+              flush=True)
         assert err <= tol
     assert abs(d["omega"] - r["omega"]) <= loops * 1e-5
 

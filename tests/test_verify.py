@@ -51,6 +51,20 @@ def test_oracle_check_pass_fail_and_missing():
     assert verify.oracle_check(["aa", "bb"], (4, 4, 16), 2, g) == "no golden"
 
 
+def test_oracle_check_noise_tables_first():
+    """oracle_check_noise compares digests only when every rank's device
+    Box-Muller tables hash like the ones the committed digests were made with."""
+    key = verify.NOISE_PREFIX + verify.golden_key((4, 4, 8), 2)
+    g = {key: {"slabs": ["aa", "bb"]}, verify.BM_TABLES_KEY: {"blake2b": "tt"}}
+    assert verify.oracle_check_noise(["aa", "bb"], ["tt", "tt"], (4, 4, 8), 2, g) == "pass"
+    assert verify.oracle_check_noise(["aa", "xx"], ["tt", "tt"], (4, 4, 8), 2, g) == "fail"
+    assert verify.oracle_check_noise(["aa", "bb"], ["tt", "tu"], (4, 4, 8), 2, g) == "tables differ"
+    assert verify.oracle_check_noise(["aa", "bb"], ["tt", "tt"], (4, 4, 16), 2, g) == "no golden"
+    assert verify.oracle_check_noise(["aa", "bb"], ["tt", "tt"], (4, 4, 8), 2, {key: g[key]}) == "no golden"
+    # the noise-off verdict never reads the noise digests
+    assert verify.oracle_check(["aa", "bb"], (4, 4, 8), 2, g) == "no golden"
+
+
 def test_committed_oracle_digests_cover_the_driver_configs():
     """tests/golden/oracle_slabs.json: weak 256^3 per GPU and strong 1024^3 at
     N = 1, 2, 4, 8, one oracle digest per rank, noise off."""
