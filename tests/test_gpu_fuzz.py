@@ -13,12 +13,12 @@ import pytest
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
 
-from conftest import tol_report
+from conftest import PHI4_STEP_ATOL, PHI4_STEP_RTOL, tol_report
 
 pytestmark = pytest.mark.gpu
 
-STEP_ATOL = 4e-6
-STEP_RTOL = 2.5e-7
+STEP_ATOL = PHI4_STEP_ATOL   # conftest.py: the measured bound (round 6)
+STEP_RTOL = PHI4_STEP_RTOL
 FUZZ = settings(max_examples=40, deadline=None, derandomize=True,
                 suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
 

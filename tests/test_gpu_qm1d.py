@@ -17,6 +17,9 @@ from conftest import golden
 
 pytestmark = pytest.mark.gpu
 
+QM1D_TOL_PER_SIGMA = 1.1e-6   # |f, x, xx0 - oracle| <= this * sig (test_frame_within_tolerance)
+QM1D_OMEGA_TOL = 4e-4         # omega after the frame
+
 
 def _gpu_frame(N, a, h, pot, C, loops, seed, f, x, xx0, omega, runs=0, lrgEl=0, lrgVl=0.0, tick=0):
     from stochquant_amd import Qm1dChain
@@ -63,13 +66,21 @@ def test_frame_within_tolerance(gpu, oracle_mod, N, pot, C):
     r = oracle_mod.qm1d_frame(N, a, h, pot, C, loops, 21, 0, 3, f, x, xx0, om, 0, 1.0)
     assert r["stable"] == 1 and stable
     sig = C * np.sqrt(np.float32(2 * h / a))
-    tol = loops * (sig * 1.4e-5 + 2e-6)
+    # the only difference is the device normals' error (the double-evaluated
+    # oracle's vs v_log/v_sqrt/v_cos), entering as sig * dxi per step; the
+    # frame's f, x, xx0 stay within QM1D_TOL_PER_SIGMA * sig (measured max
+    # 5.6e-8 at sig = 0.2 over these cases, profiles/r06/c2/tol.txt: the bound
+    # 2.2e-7 is 3.9x that; round 5's loops * (sig * 1.4e-5 + 2e-6) had
+    # ~3,000x), and C = 0 is bit-identical
+    tol = QM1D_TOL_PER_SIGMA * sig
     for k in ("f", "x", "xx0"):
         err = np.max(np.abs(d[k] - r[k]))
         print(f"TOL qm1d_frame N={N} pot={pot} C={C} {k} max_err={err:.4e} sig={sig:.4e} loops={loops} tol={tol:.4e}",
               flush=True)
         assert err <= tol
-    assert abs(d["omega"] - r["omega"]) <= loops * 1e-5
+    dom = abs(d["omega"] - r["omega"])
+    print(f"TOL qm1d_frame N={N} pot={pot} C={C} omega max_err={dom:.4e} tol={QM1D_OMEGA_TOL:.4e}", flush=True)
+    assert dom <= QM1D_OMEGA_TOL
 
 
 @pytest.mark.parametrize("N,pot,C", [(200, 0, 1.0), (1000, 0, 1.0), (200, 3, 1.0), (4096, 3, 1.0),
