@@ -21,3 +21,5 @@ for c in single rccl p2p; do
 done
 python3 scripts/r06/slab_budget.py $(find $O/tr_single -name "*kernel_trace.csv") $(find $O/tr_rccl -name "*kernel_trace.csv") \
   $(find $O/tr_p2p -name "*kernel_trace.csv") > $O/budget.txt 2>&1; tail -40 $O/budget.txt
+timeout -k 10 200 python3 scripts/r06/frames_diag.py > $O/frames_diag.log 2>&1 || { tail -20 $O/frames_diag.log; exit 5; }
+cat $O/frames_diag.log

@@ -40,6 +40,7 @@ def summarize(path, steps_per_block=16, nblk=8):
 
 def main():
     single = sys.argv[1]
+    steps_per_block = 16
     ks, phi, _, qa, la, t_end = summarize(single)
     # single slab: mean launch period of the last 80 launches (2 steps each)
     tail = la[-80:]

@@ -71,7 +71,7 @@ struct Slab {
     hipStream_t sA = nullptr, sB = nullptr;
     hipEvent_t evC = nullptr;                 // C: the block's halo exchange done
     hipEvent_t evE = nullptr;                 // E: the block's output edge planes (what the next exchange sends) done
-    float *stage = nullptr;                   // 2 G planes: the staged copy of the edge planes an exchange sends
+    float *stage = nullptr;                   // 2 G planes (x stage_slots): the staged copy of the edge planes an exchange sends
     hipEvent_t evS = nullptr;                 // S: the staged copy is complete (the field's edges may change)
     std::vector<hipEvent_t> evk;              // the block plan's SIGNAL / WAIT slots (kPlanSlots)
 };
@@ -85,9 +85,11 @@ struct EvPair {
 // number that only grows, so a wait is ">= this exchange / collective".
 constexpr int kMbStagedFromDn = 0;  // the lower neighbour's staged edge planes of exchange e are complete
 constexpr int kMbStagedFromUp = 1;  // ... the upper neighbour's
-constexpr int kMbAckFromDn = 2;     // the lower neighbour has finished reading our staged copy of exchange e
+constexpr int kMbAckFromDn = 2;     // the lower neighbour has finished reading our staged copies (teardown)
 constexpr int kMbAckFromUp = 3;     // ... the upper neighbour
 constexpr int kMbColl = 16;         // + q: rank q's contribution to collective k is in our slot q
+// staged copies per slab: P2P double-buffers them by exchange parity
+inline size_t stage_slots(int comm) { return comm == SQ_COMM_P2P ? 2 : 1; }
 constexpr int kMbWords = 1024;
 constexpr int kP2pMaxRanks = kMbWords - kMbColl;
 constexpr unsigned int kP2pMagic = 0x53513250u;  // "SQ2P"
@@ -781,19 +783,30 @@ int phi4_block(sq_ctx *c, int g) {
     }
     const bool p2p = c->p.comm == SQ_COMM_P2P;
     if (p2p && !c->p2p_ready) return fail(SQ_E_STATE, "SQ_COMM_P2P context not connected (sq_p2p_connect)");
+    // P2P: this exchange's staged slot (two, by parity).  Reusing slot e & 1 at
+    // exchange e needs both neighbours to have pulled our exchange e - 2; each
+    // wrote its staged flag of exchange e - 1 behind that pull (stream order on
+    // its exchange stream), and our exchange e - 1 waited for both flags before
+    // anything of exchange e is issued behind it -- no acknowledgement words
+    // and no waits on them per exchange (sq_destroy still drains with them).
+    const size_t slot_stride = 2 * (size_t)c->gpad * plane;
+    const size_t slot = p2p ? (size_t)((c->xchg_seq + 1) & 1u) * slot_stride : 0;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        if (plans[i][0].lo != 1 && !p2p) continue;  // P2P: the neighbours always read the staged copy
+        const bool staged_wait = plans[i][0].lo == 1;  // core pair 1 waits for the copy (WAIT_STAGED)
+        if (!staged_wait && !p2p) continue;            // P2P: the neighbours always read the staged copy
         if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
-        if (p2p && c->xchg_seq > 0) {  // both neighbours have read the previous exchange's copy
-            SQ_HIP(wait_seq(s.sB, c->mbox + kMbAckFromDn, c->xchg_seq));
-            SQ_HIP(wait_seq(s.sB, c->mbox + kMbAckFromUp, c->xchg_seq));
+        float *stg = s.stage + slot;
+        if (s.nz >= 2 * G) {  // both edge ranges in one 2-D copy (rows nz - G planes apart)
+            SQ_HIP(hipMemcpy2DAsync(stg, gbytes, src_lo[i], (size_t)(s.nz - G) * plane * sizeof(float), gbytes, 2,
+                                    hipMemcpyDeviceToDevice, s.sB));
+        } else {
+            SQ_HIP(hipMemcpyAsync(stg, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
+            SQ_HIP(hipMemcpyAsync(stg + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
         }
-        SQ_HIP(hipMemcpyAsync(s.stage, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
-        SQ_HIP(hipMemcpyAsync(s.stage + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
-        SQ_HIP(hipEventRecord(s.evS, s.sB));
-        src_lo[i] = s.stage;
-        src_hi[i] = s.stage + (size_t)G * plane;
+        if (staged_wait) SQ_HIP(hipEventRecord(s.evS, s.sB));
+        src_lo[i] = stg;
+        src_hi[i] = stg + (size_t)G * plane;
     }
     if (c->p.comm == SQ_COMM_LOOPBACK) {
         for (int i = 0; i < ns; ++i) {
@@ -825,11 +838,10 @@ int phi4_block(sq_ctx *c, int g) {
         SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
         SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
         SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromDn, e));
-        SQ_HIP(hipMemcpyAsync(p0 - n, c->peers[dn].stage + n, gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(hipMemcpyAsync(p0 - n, c->peers[dn].stage + slot + n, gbytes, hipMemcpyDeviceToDevice, s.sB));
         SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromUp, e));
-        SQ_HIP(hipMemcpyAsync(p0 + (size_t)s.nz * plane, c->peers[up].stage, gbytes, hipMemcpyDeviceToDevice, s.sB));
-        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbAckFromUp, e, 0));
-        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbAckFromDn, e, 0));
+        SQ_HIP(hipMemcpyAsync(p0 + (size_t)s.nz * plane, c->peers[up].stage + slot, gbytes, hipMemcpyDeviceToDevice,
+                              s.sB));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     } else {  // RCCL: one slab per process; this send/recv order pairs correctly for P = 2 too
@@ -1253,7 +1265,11 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipEventCreateWithFlags(&s.evS, hipEventDisableTiming));
         s.evk.assign(kPlanSlots, nullptr);
         for (hipEvent_t &e : s.evk) SQ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        if (p.comm != SQ_COMM_NONE) SQ_HIP(hipMalloc(&s.stage, 2 * (size_t)c->gpad * plane * sizeof(float)));
+        // the staged copy of the 2 G edge planes; P2P keeps two, by exchange parity
+        // (phi4_block: a neighbour's staged flag of exchange e-1 then implies it
+        // has read our copy of exchange e-2, so no per-exchange acknowledgement)
+        if (p.comm != SQ_COMM_NONE)
+            SQ_HIP(hipMalloc(&s.stage, stage_slots(p.comm) * 2 * (size_t)c->gpad * plane * sizeof(float)));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         SQ_HIP(hipEventRecord(s.evE, s.sA));
     }
@@ -2103,8 +2119,14 @@ int sq_destroy(sq_ctx *c) {
         // P2P: our staged copy may still be read by a neighbour that is behind;
         // free it only after both have acknowledged the last exchange (bounded
         // wait: a peer that died leaves the buffers mapped, not a hang)
+        // (exchanges do not acknowledge one by one, phi4_block: the last one is
+        // acknowledged here, behind our own pulls of it on the exchange stream)
         hipStream_t sB = c->slabs[0].sB;
-        if (wait_seq(sB, c->mbox + kMbAckFromDn, c->xchg_seq) != hipSuccess ||
+        const int P = c->p.nranks, r = c->p.rank;
+        const int up = (r + 1) % P, dn = (r + P - 1) % P;
+        if (hipStreamWriteValue32(sB, c->peers[dn].mbox + kMbAckFromUp, c->xchg_seq, 0) != hipSuccess ||
+            hipStreamWriteValue32(sB, c->peers[up].mbox + kMbAckFromDn, c->xchg_seq, 0) != hipSuccess ||
+            wait_seq(sB, c->mbox + kMbAckFromDn, c->xchg_seq) != hipSuccess ||
             wait_seq(sB, c->mbox + kMbAckFromUp, c->xchg_seq) != hipSuccess)
             p2p_drained = false;
         const auto t0 = std::chrono::steady_clock::now();
