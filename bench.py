@@ -24,7 +24,7 @@ Roofline: the dominant kernel is the two-step fused kernel,
 which moves the field once per two updates and is bound by VALU issue, not
 HBM.  `bound` "valu", `frac` = the launch's VALU-busy SIMD cycles (4 x
 SQ_ACTIVE_INST_VALU from the committed rocprofv3 PMC record of this same
-command, profiles/r05/driver_profile.json) / (1024 SIMDs x 2.4 GHz x the launch
+command, profiles/r06/driver_profile.json) / (1024 SIMDs x 2.4 GHz x the launch
 time measured here with dispatch events, as rocprofv3's kernel trace measures
 it).  Beside it: `frac_algorithmic` (8 B per site update, SURVEY.md §8d, over
 the same time -- saturates by construction under two-step temporal blocking),
@@ -246,7 +246,7 @@ def cpu_baseline(L, dtau, target_s):
                       f"{cores} threads = this job's CPU share of {os.cpu_count()} host CPUs), {dt:.2f} s"}
 
 
-PROFILE = os.path.join("profiles", "r05", "driver_profile.json")
+PROFILE = os.path.join("profiles", "r06", "driver_profile.json")
 PROFILE_TIMING_TOL = 0.03       # the record's rocprof launch time must be within 3 % of this run's
 N_SIMD = 1024                   # 256 CUs x 4 SIMDs
 CLOCK_MHZ = 2400.0              # peak engine clock (MI355X_MICROARCH.md)
@@ -261,7 +261,7 @@ def short_kernel(name):
 
 def pmc_record(L, launched, build, path=None):
     """The committed rocprofv3 record of the driver's invocation for this lattice
-    (profiles/r05/driver_profile.json, made by scripts/r05_driver_prof.sh +
+    (profiles/r06/driver_profile.json, made by scripts/r06/driver_prof.sh +
     scripts/driver_profile.py from `python3 bench.py --steps 20 --warmup 5`,
     not measured inside this run): PMC HBM bytes and VALU-busy cycles per launch
     of the fused kernel, and its rocprof dispatch durations.
@@ -538,11 +538,14 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
         # divided by the live launch time above; its rocprof durations describe
         # this run only when they agree with the live launch (within
         # PROFILE_TIMING_TOL) -- otherwise they are flagged and not quoted
-        ratio = launch_ms * 1e3 / rec["rocprof_avg_us"] if rec.get("rocprof_avg_us") else None
+        # the record's launches after the settle phase when it has them (the
+        # state the roofline pass runs in), else all of them
+        rp_us = rec.get("rocprof_steady_avg_us") or rec.get("rocprof_avg_us")
+        ratio = launch_ms * 1e3 / rp_us if rp_us else None
         mismatch = ratio is not None and abs(ratio - 1.0) > PROFILE_TIMING_TOL
         keys = ["valu_busy_cycles_per_launch", "valu_insts_per_wave", "avg_resident_waves_per_simd"]
         if not mismatch:
-            keys += ["rocprof_avg_us", "rocprof_median_us", "valu_util_simd_at_rocprof_avg"]
+            keys += ["rocprof_avg_us", "rocprof_steady_avg_us", "rocprof_median_us", "valu_util_simd_at_rocprof_avg"]
         for k in keys:
             if rec.get(k) is not None:
                 r["profile_" + k] = rec[k]

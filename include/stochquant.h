@@ -264,6 +264,11 @@ int sq_correlator(sq_ctx *ctx, double *out, int n);
 int sq_set_profiling(sq_ctx *ctx, int mode);
 int sq_perf(sq_ctx *ctx, sq_perf_t *out);
 int sq_perf_reset(sq_ctx *ctx);
+/* Joins the context's streams and reports asynchronous errors.  A slab
+ * exchange whose gated rim chunks timed out (SQ_E_COMM) is sticky: the
+ * field's rim planes are stale, so sq_sync, sq_download_field, sq_step and
+ * the frame calls keep failing with it until sq_upload_field / sq_load_field
+ * / sq_init_field(_hash) replaces the field. */
 int sq_sync(sq_ctx *ctx);
 /* PHI4: the step kernel launched most often since the last sq_perf_reset, as
  * its template instance (e.g. "phi4_tb2_kernel<true, false, 1, false, true,
