@@ -538,14 +538,11 @@ def roofline(a, lat, L, world, slab_path, t, perf, nslabs, sites_local):
         # divided by the live launch time above; its rocprof durations describe
         # this run only when they agree with the live launch (within
         # PROFILE_TIMING_TOL) -- otherwise they are flagged and not quoted
-        # the record's launches after the settle phase when it has them (the
-        # state the roofline pass runs in), else all of them
-        rp_us = rec.get("rocprof_steady_avg_us") or rec.get("rocprof_avg_us")
-        ratio = launch_ms * 1e3 / rp_us if rp_us else None
+        ratio = launch_ms * 1e3 / rec["rocprof_avg_us"] if rec.get("rocprof_avg_us") else None
         mismatch = ratio is not None and abs(ratio - 1.0) > PROFILE_TIMING_TOL
         keys = ["valu_busy_cycles_per_launch", "valu_insts_per_wave", "avg_resident_waves_per_simd"]
         if not mismatch:
-            keys += ["rocprof_avg_us", "rocprof_steady_avg_us", "rocprof_median_us", "valu_util_simd_at_rocprof_avg"]
+            keys += ["rocprof_avg_us", "rocprof_median_us", "valu_util_simd_at_rocprof_avg"]
         for k in keys:
             if rec.get(k) is not None:
                 r["profile_" + k] = rec[k]

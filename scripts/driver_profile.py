@@ -1,5 +1,5 @@
 """Summarise rocprofv3 runs of the DRIVER's bench invocation into the record
-bench.py's roofline reads (profiles/r06/driver_profile.json).
+bench.py's roofline reads (profiles/r0N/driver_profile.json: r05, r06).
 
 Inputs (one rocprofv3 run each, all of `python3 bench.py --steps 20 --warmup 5`,
 MI355X_MICROARCH.md §rocprofv3: counters in passes of their own):
@@ -15,8 +15,7 @@ record carries the library's build id (sq_build_id: the hash of the φ⁴
 kernels' code object), so bench.py uses it only for that binary.  Per launch:
   * rocprof_avg_us / rocprof_median_us: dispatch durations from the trace
     (every launch of that kernel and grid in the run: settle, warm-up, timed,
-    roofline pass); rocprof_steady_avg_us: the launches after the settle
-    phase only (the record's timing bench.py compares with its live launch);
+    roofline pass);
   * hbm_bytes_per_launch: FETCH_SIZE x 2 (gfx950: wide streaming reads are
     counted at half their bytes) + WRITE_SIZE, KiB x 1024, medians;
   * valu_busy_cycles_per_launch: SQ_ACTIVE_INST_VALU x 4 (quad-cycles), the
@@ -50,30 +49,16 @@ def _rows(d, pat):
             yield from csv.DictReader(fh)
 
 
-SETTLE_S = 1.6   # bench.py's clock-settle phase (--settle-ms 1500) after a lattice's first launch
-
-
 def fused_groups(trace_dir):
-    """{(kernel, grid): [durations us]} of the fused step kernels in the trace,
-    and {(kernel, grid): [durations us]} of the same launches after the first
-    SETTLE_S seconds of each group (the state bench.py's timed region and
-    roofline pass run in: the settle phase's launches alternate 25-launch
-    batches with host synchronisations)."""
-    g, t = {}, {}
+    """{(kernel, grid): [durations us]} of the fused step kernels in the trace."""
+    g = {}
     for r in _rows(trace_dir, "*kernel_trace.csv"):
         k = r["Kernel_Name"]
         if "phi4_tb2" not in k:
             continue
         grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        s0, s1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        g.setdefault((k, grid), []).append((s1 - s0) * 1e-3)
-        t.setdefault((k, grid), []).append((s0, (s1 - s0) * 1e-3))
-    steady = {}
-    for key, v in t.items():
-        v.sort()
-        t0 = v[0][0]
-        steady[key] = [d for s, d in v if s - t0 > SETTLE_S * 1e9] or [d for _, d in v]
-    return g, steady
+        g.setdefault((k, grid), []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3)
+    return g
 
 
 def counters(d, kernel, grid):
@@ -96,7 +81,7 @@ def main():
     ap.add_argument("--command", default="python3 bench.py --steps 20 --warmup 5")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    groups, steady = fused_groups(a.trace)
+    groups = fused_groups(a.trace)
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from stochquant_amd import _lib
@@ -114,11 +99,8 @@ def main():
         s, ns = counters(a.sq, k, grid)
         avg = statistics.fmean(durs)
         med = statistics.median(durs)
-        sd = steady[(k, grid)]
         rec = {"kernel": k, "grid": grid, "build_id_phi4": bid.get("phi4"), "launches_in_trace": len(durs),
                "rocprof_avg_us": round(avg, 3), "rocprof_median_us": round(med, 3),
-               "rocprof_steady_avg_us": round(statistics.fmean(sd), 3), "steady_launches": len(sd),
-               "steady_is": f"launches more than {SETTLE_S} s after the group's first (after bench.py's settle phase)",
                "rocprof_min_us": round(min(durs), 3), "sites": size ** 3, "steps_per_launch": 2,
                "algorithmic_bytes_per_launch": 8 * size ** 3 * 2, "hbm_min_bytes_per_launch": 8 * size ** 3}
         if "FETCH_SIZE" in f and "WRITE_SIZE" in w:

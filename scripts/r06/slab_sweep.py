@@ -13,7 +13,8 @@ import torch  # noqa: E402
 from stochquant_amd import Phi4Lattice, unique_id  # noqa: E402
 
 STEPS = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
-KNOBS = ("SQ_GHOST", "SQ_CORE_PAIRS", "SQ_RIMS_B", "SQ_EDGE_FIRST", "SQ_XCHG_BLOCKS")
+KNOBS = ("SQ_GHOST", "SQ_CORE_PAIRS", "SQ_RIMS_B", "SQ_EDGE_FIRST", "SQ_XCHG_BLOCKS", "SQ_XCHG_PRIO",
+         "SQ_EDGES_STOPEV")
 CASES = [
     ("rccl", {}),
     ("rccl", {"SQ_GHOST": "12"}), ("rccl", {"SQ_GHOST": "20"}), ("rccl", {"SQ_GHOST": "24"}),
@@ -39,9 +40,14 @@ def timed(L):
     return (time.perf_counter() - t0) * 1e6 / STEPS
 
 
+REPS = 2
 if len(sys.argv) > 2 and sys.argv[2] == "p2ponly":
     CASES = [("p2p", {}), ("rccl", {}), ("p2p", {"SQ_GHOST": "24"})]
-for rep in range(2):
+if len(sys.argv) > 2 and sys.argv[2] == "prio":
+    CASES = [("rccl", {}), ("rccl", {"SQ_XCHG_PRIO": "0"}), ("rccl", {"SQ_EDGES_STOPEV": "1"}),
+             ("rccl", {"SQ_GHOST": "12"}), ("p2p", {}), ("p2p", {"SQ_XCHG_PRIO": "0"}), ("p2p", {"SQ_GHOST": "12"})]
+    REPS = 4
+for rep in range(REPS):
     for comm, env in CASES:
         for k in KNOBS:
             os.environ.pop(k, None)

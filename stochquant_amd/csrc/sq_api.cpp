@@ -1257,9 +1257,11 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipStreamCreateWithFlags(&s.sA, hipStreamNonBlocking));
         // halo stream at the highest priority: its RCCL and boundary-plane
         // kernels must not queue behind the interior kernel's waves
+        // (SQ_XCHG_PRIO=0: the default priority, an experiment)
         int prio_lo = 0, prio_hi = 0;
         SQ_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        SQ_HIP(hipStreamCreateWithPriority(&s.sB, hipStreamNonBlocking, prio_hi));
+        const char *xp = getenv("SQ_XCHG_PRIO");
+        SQ_HIP(hipStreamCreateWithPriority(&s.sB, hipStreamNonBlocking, (xp && atoi(xp) == 0) ? prio_lo : prio_hi));
         SQ_HIP(hipEventCreateWithFlags(&s.evC, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evE, hipEventDisableTiming));
         SQ_HIP(hipEventCreateWithFlags(&s.evS, hipEventDisableTiming));
