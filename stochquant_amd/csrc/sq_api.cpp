@@ -192,6 +192,7 @@ struct sq_ctx {
     bool fin_sync = false;     // multi-rank: field_finite changed locally; the next step call
                                // agrees on it across ranks first (ghost planes come from neighbours)
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0|1 pins it)
+    bool diag_no_xwait = false;  // SQ_DIAG_NO_XWAIT: timing diagnostics only (results wrong)
     bool ef_auto = true;    // the timed pick also tries the other edge_first (unless SQ_EDGE_FIRST pins it)
     int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
     bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
@@ -797,13 +798,10 @@ int phi4_block(sq_ctx *c, int g) {
         if (!staged_wait && !p2p) continue;            // P2P: the neighbours always read the staged copy
         if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
         float *stg = s.stage + slot;
-        if (s.nz >= 2 * G) {  // both edge ranges in one 2-D copy (rows nz - G planes apart)
-            SQ_HIP(hipMemcpy2DAsync(stg, gbytes, src_lo[i], (size_t)(s.nz - G) * plane * sizeof(float), gbytes, 2,
-                                    hipMemcpyDeviceToDevice, s.sB));
-        } else {
-            SQ_HIP(hipMemcpyAsync(stg, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
-            SQ_HIP(hipMemcpyAsync(stg + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
-        }
+        // two linear copies: one 2-D copy of both ranges ran as a rect-copy kernel
+        // of 23 us against 2 x 6 (profiles/r06/c6/tr_p2p)
+        SQ_HIP(hipMemcpyAsync(stg, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
+        SQ_HIP(hipMemcpyAsync(stg + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
         if (staged_wait) SQ_HIP(hipEventRecord(s.evS, s.sB));
         src_lo[i] = stg;
         src_hi[i] = stg + (size_t)G * plane;
@@ -922,7 +920,8 @@ int phi4_block(sq_ctx *c, int g) {
                 c->stop_next = nullptr;  // an empty range launched nothing: EDGES_DONE records
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
                 if (op.stream != kB) xchg_live = false;
-                if (op.stream != kB) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));  // B: ordered behind its exchange
+                // (SQ_DIAG_NO_XWAIT=1, timing diagnostics only: no wait, the rims race the exchange)
+                if (op.stream != kB && !c->diag_no_xwait) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));
                 if (c->p.comm == SQ_COMM_LOOPBACK) {
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + ns - 1) % ns].evC, 0));
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + 1) % ns].evC, 0));
@@ -1350,12 +1349,12 @@ int create_phi4(sq_ctx *c) {
     while (zc > 1 && rows * ((nz_max + zc - 1) / zc) < 2048) zc /= 2;
     while (zc < 32 && rows * ((nz_max + 2 * zc - 1) / (2 * zc)) >= 32768) zc *= 2;
     if (const char *e = getenv("SQ_ZCHUNK")) zc = std::max(1, atoi(e));
-    // edges-first by default except for one rank's RCCL self-exchange, which is
-    // short enough to fit beside the next core pair (off: 19.2-19.4 vs 19.9
-    // us/step; the P2P self-exchange's flag round trips want the early start:
-    // 20.9-21.1 off vs 20.2-20.4 on); the timed pick of multi-rank contexts
-    // tries both
-    c->edge_first = !(c->p.comm == SQ_COMM_RCCL && c->p.nranks == 1);
+    // edges-first by default except for one rank's self-exchange, which is short
+    // enough to fit beside the next core pair: RCCL (off 19.2-19.4 vs 19.9
+    // us/step, round 3) and, since round 6's shorter P2P chain, P2P (off 1.180
+    // vs 1.201 x the single slab, profiles/r06/c7/slab_ab.log); the timed pick
+    // of multi-rank contexts tries both
+    c->edge_first = !((c->p.comm == SQ_COMM_RCCL || c->p.comm == SQ_COMM_P2P) && c->p.nranks == 1);
     if (const char *e = getenv("SQ_EDGE_FIRST")) {
         c->edge_first = atoi(e) != 0;
         c->ef_auto = false;
@@ -1403,6 +1402,7 @@ int create_phi4(sq_ctx *c) {
         c->tb_blocks_xchg = std::max(1, c->tb_blocks - 96);
         if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
         if (const char *e = getenv("SQ_EDGES_STOPEV")) c->edges_stopev = atoi(e) != 0;
+        if (const char *e = getenv("SQ_DIAG_NO_XWAIT")) c->diag_no_xwait = atoi(e) != 0;
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
