@@ -678,87 +678,116 @@ def c1_record(a, local):
     }
 
 
-def frames_record(a, local, nframes=100, loops=20):
+def frames_record(a, local, nframes=100, loops=20, rounds=4):
     """tauhost.c:479-560's unit on the north-star lattice: 20-step 256^3 frames
     (guard, stability rule, rollback, Δτ controller) decided on the device
-    (sq_run_frames), in one batch of `nframes`, against raw 20-step blocks
-    (sq_step) in the same context and run."""
+    (sq_run_frames), against raw 20-step blocks (sq_step) in the same context
+    and run: `rounds` alternating rounds of a batch of nframes / rounds frames
+    and as many raw steps, summed per kind (one batch of frames timed before
+    one block of raw steps put 1-4 points of clock-state difference into the
+    overhead, round 6, scripts/r06/frames_diag.py)."""
+    import numpy as np
     import torch
     from stochquant_amd import Phi4Lattice
+    per = nframes // rounds
     with Phi4Lattice((256, 256, 256), dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local, loops=loops) as L:
         L.init_field(0.1)
         L.run_frames(20)                   # warm-up: code objects, the controller, clocks
         L.step(200)
         L.sync()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        st, dts = L.run_frames(nframes)
-        L.sync()
-        tf = time.perf_counter() - t0
-        L.step(400)
-        L.sync()
-        nraw = nframes * loops
-        t0 = time.perf_counter()
-        L.step(nraw)
-        L.sync()
-        tr = time.perf_counter() - t0
+        tf = tr = 0.0
+        sts, dts = [], []
+        for _ in range(rounds):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st, dt = L.run_frames(per)
+            L.sync()
+            tf += time.perf_counter() - t0
+            sts.append(st)
+            dts.append(dt)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            L.step(per * loops)
+            L.sync()
+            tr += time.perf_counter() - t0
         m = L.moments()
-    us_f = tf * 1e6 / nframes
-    us_raw = tr * 1e6 / nraw * loops
+    nf = per * rounds
+    st, dts = np.concatenate(sts), np.concatenate(dts)
+    us_f = tf * 1e6 / nf
+    us_raw = tr * 1e6 / (nf * loops) * loops
     return {"config": {"workload": "phi^4 256^3 fp32, frames of 20 Langevin steps through sq_run_frames (the "
                                    "frame loop of tauhost.c:479-560 on the device: guard flag, stability rule, "
-                                   "rollback, Δτ controller)", "loops": loops, "frames": nframes,
+                                   "rollback, Δτ controller)", "loops": loops, "frames": nf, "rounds": rounds,
+                       "method": "alternating rounds of a frame batch and as many raw steps, summed per kind",
                        "dtau0": a.dtau, "m2": 1.0, "lambda": 1.0},
             "us_per_frame": round(us_f, 2), "raw_us_per_20_steps": round(us_raw, 2),
             "overhead": round(us_f / us_raw - 1.0, 4), "stable_frames": int(st.sum()),
             "dtau_final": float(dts[-1]) if len(dts) else None,
-            "value": 256 ** 3 * loops * nframes / tf, "unit": "site-updates/s (frames)",
+            "value": 256 ** 3 * loops * nf / tf, "unit": "site-updates/s (frames)",
             "field_check": {"maxabs": m["maxabs"]}}
 
 
-def slab_record(a, local, steps=1000):
+def slab_record(a, local, steps=1000, rounds=5):
     """SURVEY §8e's slab path on one GPU: the 256^3 lattice as one z-slab whose
     halo exchange goes through the product's transports to itself (RCCL
     self-exchange; P2P peer pointers), G = 16 deep halos, fused pairs, the
     exchange on stream B -- per-step time against the single periodic slab in
     the same run (the ratio is what the exchange machinery costs before any
-    xGMI)."""
+    xGMI).  All three contexts stay open and are timed in turn, `rounds` times
+    `steps` steps each after 2000 warm-up steps, medians: one measurement per
+    context right after its creation read the single slab 2-5 % slow or fast
+    with the clock state (round 6, scripts/r06/slab_ab.py)."""
+    import statistics
     import torch
     from stochquant_amd import Phi4Lattice, unique_id
     kw = dict(dtau=a.dtau, m2=1.0, lam=1.0, seed=0x5EED, device=local)
-    out = {}
+    out, ctxs = {}, {}
 
-    def timed(L):
-        L.init_field(0.1)
-        L.step(400)
-        L.sync()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        L.step(steps)
-        L.sync()
-        return (time.perf_counter() - t0) * 1e6 / steps
-
-    for name, mk in (("single", lambda: Phi4Lattice((256, 256, 256), **kw)),
-                     ("rccl", lambda: Phi4Lattice((256, 256, 256), comm="rccl", nranks=1, rank=0,
-                                                  comm_id=unique_id(), **kw)),
-                     ("p2p", lambda: Phi4Lattice((256, 256, 256), comm="p2p", nranks=1, rank=0, **kw))):
+    def p2p():
+        L = Phi4Lattice((256, 256, 256), comm="p2p", nranks=1, rank=0, **kw)
         try:
-            with mk() as L:
-                if name == "p2p":
-                    L.p2p_connect([L.p2p_handle()])
-                us = timed(L)
-                sch = L.schedule if name != "single" else None
-            out[name] = {"us_per_step": round(us, 3)}
-            if sch:
-                out[name]["schedule"] = sch
-        except Exception as e:   # the headline record stands without it
-            out[name] = {"error": str(e)[:200]}
+            L.p2p_connect([L.p2p_handle()])
+        except Exception:
+            L.close()
+            raise
+        return L
+
+    try:
+        for name, mk in (("single", lambda: Phi4Lattice((256, 256, 256), **kw)),
+                         ("rccl", lambda: Phi4Lattice((256, 256, 256), comm="rccl", nranks=1, rank=0,
+                                                      comm_id=unique_id(), **kw)),
+                         ("p2p", p2p)):
+            try:
+                L = mk()
+                L.init_field(0.1)
+                L.step(2000)
+                L.sync()
+                ctxs[name] = L
+            except Exception as e:   # the headline record stands without it
+                out[name] = {"error": str(e)[:200]}
+        times = {n: [] for n in ctxs}
+        for _ in range(rounds):
+            for n, L in ctxs.items():
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                L.step(steps)
+                L.sync()
+                times[n].append((time.perf_counter() - t0) * 1e6 / steps)
+        for n, L in ctxs.items():
+            out[n] = {"us_per_step": round(statistics.median(times[n]), 3),
+                      "us_per_step_rounds": [round(t, 3) for t in times[n]]}
+            if n != "single":
+                out[n]["schedule"] = L.schedule
+    finally:
+        for L in ctxs.values():
+            L.close()
     base = out.get("single", {}).get("us_per_step")
     for name in ("rccl", "p2p"):
-        if base and "us_per_step" in out[name]:
+        if base and "us_per_step" in out.get(name, {}):
             out[name]["ratio_to_single"] = round(out[name]["us_per_step"] / base, 4)
     out["config"] = {"workload": "phi^4 256^3 fp32 as one z-slab with self-exchange (RCCL / P2P), one GPU",
-                     "steps": steps}
+                     "steps": steps, "rounds": rounds,
+                     "method": "three open contexts timed in turn, medians of the rounds"}
     return out
 
 

@@ -721,11 +721,12 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
     // block has read it.  (One shared word let a block that left barrier j+2
     // early overwrite tag j+1 with j+2 before a slower block had read it.)  The
     // copies: ds[N] bytes 0 and 24 (the barrier counter sits at byte 16).
+    // (the copy of parity q is lw + 3 q: an address by arithmetic, not an array
+    // of two pointers indexed by the step, which would live in private memory)
     unsigned long long *lw = reinterpret_cast<unsigned long long *>(A.ds + N), *unst = lw + 1;
-    unsigned long long *lead[2] = {lw, lw + 3};
     if (gt == 0) {  // write-through: the other blocks' atomics (and, SC1, loads) must see the zeros
-        __hip_atomic_store(lead[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(lead[1], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(lw + 3, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(unst, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     double nx[kGridK], nxx0[kGridK], D[kGridK];
@@ -870,7 +871,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
         // 2a. the outcome of step j-1's scan
         if (j > 0) {
             const unsigned long long tag = (unsigned long long)j;
-            const unsigned long long lv = __hip_atomic_load(lead[j & 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned long long lv = __hip_atomic_load(lw + 3 * (j & 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((lv >> 32) == tag) E = (int)(lv & 0xffffffffull) - 1;
             V = totA;
             steps = j;
@@ -904,7 +905,7 @@ __global__ __launch_bounds__(kGridT) void qm1d_frame_grid(const Qm1dArgs A) {
             runA = fmax(runA, absol(X[k]));
         }
         const unsigned long long tag1 = (unsigned long long)(j + 1);
-        if (leader >= 0) atomicMax(lead[(j + 1) & 1], (tag1 << 32) | (unsigned long long)(leader + 1));
+        if (leader >= 0) atomicMax(lw + 3 * ((j + 1) & 1), (tag1 << 32) | (unsigned long long)(leader + 1));
         if (un) atomicMax(unst, tag1);
         myLead = leader;
         stamp(j, 4);
