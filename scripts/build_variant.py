@@ -30,7 +30,7 @@ def main():
     finally:
         os.remove(dst_src)
     objs = [obj] + [os.path.join(build.OBJ, s + ".o") for s in build.DEVICE_SOURCES + build.HOST_SOURCES
-                    if s != which]
+                    if s != which] + [os.path.join(build.OBJ, "sq_build_id.cpp.o")]  # the base build's identity
     out = os.path.join(build.LIBDIR, "variants", f"libstochquant_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     subprocess.run([build.HIPCC, f"--offload-arch={build.ARCH}", "-shared", "-fPIC", "-o", out] + objs
