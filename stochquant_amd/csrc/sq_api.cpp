@@ -239,6 +239,7 @@ struct sq_ctx {
     sq::FrameCtl *ctl_cur = nullptr;
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
     bool tbz_pin = false;           // SQ_FUSE2_Z pinned the planes per block
+    int tb_minz = 4;                // fewest planes per block of a fused launch (SQ_TB2_MINZ, an experiment)
     int tb_blocks = 512;            // otherwise: blocks per launch aimed at (two per CU)
     // slab paths: the fused launches that run beside an exchange (the core
     // pairs, the middle pair after EDGES_DONE) aim at fewer blocks: the
@@ -555,7 +556,7 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     // (the slabs of a loopback decomposition run concurrently on their own streams)
     const int target = c->beside_xchg ? c->tb_blocks_xchg : c->tb_blocks;
     const int nzc_t = std::max(1, target / (nyg * nxseg * (int)c->slabs.size() * nr));
-    const int zb = c->tbz_pin ? c->tbz : std::min(len, std::max(4, (len + nzc_t - 1) / nzc_t));
+    const int zb = c->tbz_pin ? c->tbz : std::min(len, std::max(c->tb_minz, (len + nzc_t - 1) / nzc_t));
     a.zlo = lo;
     a.zhi = nr == 2 ? hi2 : hi;
     a.zstep = nr == 2 ? lo2 - lo : 0;
@@ -1387,6 +1388,7 @@ int create_phi4(sq_ctx *c) {
     const bool fuse = fe ? atoi(fe) != 0 : p.comm != SQ_COMM_LOOPBACK;
     if (fuse && sq::phi4_tb2_supported(c->Lx, c->Ly) && (p.comm != SQ_COMM_NONE || c->slabs[0].nz >= 2)) {
         c->tbz = 16;
+        if (const char *z = getenv("SQ_TB2_MINZ")) c->tb_minz = std::max(1, atoi(z));
         if (const char *z = getenv("SQ_FUSE2_Z")) {
             c->tbz = std::max(1, atoi(z));
             c->tbz_pin = true;
