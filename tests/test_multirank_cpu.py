@@ -197,6 +197,8 @@ def _monolithic(steps):
     (2, 17, True, True, 8, 2, "B", False),
     (2, 19, True, True, 8, 4, "A", True),      # every pair of the block split into core and rim
     (3, 11, True, False, 8, 3, "B", True),     # three core pairs, slabs of 12 planes (the core shrinks to 4)
+    (8, 9, True, True, 2, 1, "list", False),   # the driver's N = 8: slabs of 4-5 planes, G = 2
+    (8, 9, True, True, 2, 1, "B", True),
 ])
 def test_gloo_deep_halo_blocks_bitwise(world, steps, fuse2, edge_first, gpad, core_pairs, prefer, rims_b, oracle_mod):
     ctx = mp.get_context("spawn")
