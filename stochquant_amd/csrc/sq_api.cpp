@@ -235,6 +235,10 @@ struct sq_ctx {
     bool tri = false;
     float *tri_bufs[3] = {nullptr, nullptr, nullptr};
     int frame_tk = 0;
+    // the host's guess of the current frame's buffer roles (FrameCtl::bs / bw0 /
+    // bw1 if every earlier frame of the batch was stable); SQ_FRAME_SPEC=0: off
+    int spec_bs = 0, spec_bw0 = 1, spec_bw1 = 2;
+    bool tri_spec = true;
     bool clr_first = false;         // ... armed by the next launch even without a fold (a batch's frame 0)
     sq::FrameCtl *ctl_cur = nullptr;
     int tbz = 0;                    // two-step fused launches: > 0 on; planes per block when pinned
@@ -479,6 +483,14 @@ sq::Phi4StepArgs phi4_base_args(sq_ctx *c, const Slab &s, int in_buf) {
         a.buf2 = c->tri_bufs[2];
         a.tctl = c->ctl_cur;
         a.tk = c->frame_tk++;
+        // the guess: the roles every earlier frame of the batch being stable
+        // gives (phi4_frames_dev keeps them); kernels that can start on it
+        // check it against the controller once their first loads are out
+        const int bi = a.tk == 0 ? c->spec_bs : ((a.tk & 1) ? c->spec_bw0 : c->spec_bw1);
+        const int bo = a.tk == 0 ? c->spec_bw0 : ((a.tk & 1) ? c->spec_bw1 : c->spec_bw0);
+        a.in = c->tri_bufs[bi];
+        a.out = c->tri_bufs[bo];
+        a.tspec = c->tri_spec ? 1 : 0;
     }
     return a;
 }
@@ -1925,6 +1937,13 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         h.bw1 = 2;
         h.nl_odd = ((L / 2) + (L & 1)) & 1;  // launches per frame: the pairs and an odd last step
     }
+    c->spec_bs = 0;  // the guess starts from the roles the controller starts from
+    c->spec_bw0 = 1;
+    c->spec_bw1 = 2;
+    {
+        const char *fs = getenv("SQ_FRAME_SPEC");
+        c->tri_spec = !(fs && atoi(fs) == 0);
+    }
     SQ_HIP(hipMemcpyAsync(c->ctl, c->ctl_host, sizeof h, hipMemcpyHostToDevice, st));
     // the active record set must start zero; each frame-end launch clears the
     // other one, which the next frame then uses
@@ -1963,6 +1982,13 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
             c->clr_first = true;
         }
         int rc = phi4_steps(c, L);
+        if (tri) {  // the next frame's roles if this one is stable (frame_decide's rotation)
+            const int fin = h.nl_odd ? c->spec_bw0 : c->spec_bw1;
+            const int third = 3 - c->spec_bs - fin;
+            c->spec_bw1 = c->spec_bs;
+            c->spec_bs = fin;
+            c->spec_bw0 = third;
+        }
         c->in_frame = false;
         c->dev_frames = false;
         c->snap_next = nullptr;

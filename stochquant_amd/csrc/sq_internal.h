@@ -105,6 +105,10 @@ struct Phi4StepArgs {
     float *buf0, *buf1, *buf2;  // (named fields: a dynamic index would put the argument block in private memory)
     const FrameCtl *tctl;
     int tk;
+    // tctl != nullptr and tspec: in / out hold the host's guess of launch tk's
+    // buffers (every earlier frame of the batch stable); kernels that can
+    // (phi4_tb2_kernel) start on it and check it against *tctl, others ignore it
+    int tspec;
     // slab paths, gated launch (gate != nullptr; fused kernels): the first n_reg
     // blocks are the usual chunks of the core range; the blocks after them are
     // thin chunks (tzc planes, ntz per range) of the two rim ranges [tlo0, +tlen)
