@@ -678,14 +678,14 @@ def c1_record(a, local):
     }
 
 
-def frames_record(a, local, nframes=100, loops=20, rounds=4):
+def frames_record(a, local, nframes=200, loops=20, rounds=8):
     """tauhost.c:479-560's unit on the north-star lattice: 20-step 256^3 frames
     (guard, stability rule, rollback, Δτ controller) decided on the device
     (sq_run_frames), against raw 20-step blocks (sq_step) in the same context
     and run: `rounds` alternating rounds of a batch of nframes / rounds frames
-    and as many raw steps, summed per kind (one batch of frames timed before
-    one block of raw steps put 1-4 points of clock-state difference into the
-    overhead, round 6, scripts/r06/frames_diag.py)."""
+    and as many raw steps, in alternating order, summed per kind (one batch of
+    frames timed before one block of raw steps put 1-4 points of clock-state
+    difference into the overhead, round 6, scripts/r06/frames_diag.py)."""
     import numpy as np
     import torch
     from stochquant_amd import Phi4Lattice
@@ -697,19 +697,30 @@ def frames_record(a, local, nframes=100, loops=20, rounds=4):
         L.sync()
         tf = tr = 0.0
         sts, dts = [], []
-        for _ in range(rounds):
+
+        def frames():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             st, dt = L.run_frames(per)
             L.sync()
-            tf += time.perf_counter() - t0
             sts.append(st)
             dts.append(dt)
+            return time.perf_counter() - t0
+
+        def raw():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             L.step(per * loops)
             L.sync()
-            tr += time.perf_counter() - t0
+            return time.perf_counter() - t0
+
+        for r in range(rounds):  # the order alternates too: whichever runs first after a sync reads differently
+            if r % 2 == 0:
+                tf += frames()
+                tr += raw()
+            else:
+                tr += raw()
+                tf += frames()
         m = L.moments()
     nf = per * rounds
     st, dts = np.concatenate(sts), np.concatenate(dts)
@@ -718,7 +729,7 @@ def frames_record(a, local, nframes=100, loops=20, rounds=4):
     return {"config": {"workload": "phi^4 256^3 fp32, frames of 20 Langevin steps through sq_run_frames (the "
                                    "frame loop of tauhost.c:479-560 on the device: guard flag, stability rule, "
                                    "rollback, Δτ controller)", "loops": loops, "frames": nf, "rounds": rounds,
-                       "method": "alternating rounds of a frame batch and as many raw steps, summed per kind",
+                       "method": "alternating rounds (and order) of a frame batch and as many raw steps, summed per kind",
                        "dtau0": a.dtau, "m2": 1.0, "lambda": 1.0},
             "us_per_frame": round(us_f, 2), "raw_us_per_20_steps": round(us_raw, 2),
             "overhead": round(us_f / us_raw - 1.0, 4), "stable_frames": int(st.sum()),
@@ -766,8 +777,10 @@ def slab_record(a, local, steps=1000, rounds=5):
             except Exception as e:   # the headline record stands without it
                 out[name] = {"error": str(e)[:200]}
         times = {n: [] for n in ctxs}
-        for _ in range(rounds):
-            for n, L in ctxs.items():
+        names = list(ctxs)
+        for r in range(rounds):
+            for n in names[r % len(names):] + names[:r % len(names)]:  # each context first in turn
+                L = ctxs[n]
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 L.step(steps)
@@ -787,7 +800,7 @@ def slab_record(a, local, steps=1000, rounds=5):
             out[name]["ratio_to_single"] = round(out[name]["us_per_step"] / base, 4)
     out["config"] = {"workload": "phi^4 256^3 fp32 as one z-slab with self-exchange (RCCL / P2P), one GPU",
                      "steps": steps, "rounds": rounds,
-                     "method": "three open contexts timed in turn, medians of the rounds"}
+                     "method": "three open contexts timed in turn (the order rotating), medians of the rounds"}
     return out
 
 
