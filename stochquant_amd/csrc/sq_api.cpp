@@ -90,6 +90,8 @@ constexpr int kMbAckFromUp = 3;     // ... the upper neighbour
 constexpr int kMbColl = 16;         // + q: rank q's contribution to collective k is in our slot q
 // staged copies per slab: P2P double-buffers them by exchange parity
 inline size_t stage_slots(int comm) { return comm == SQ_COMM_P2P ? 2 : 1; }
+// polls of the P2P hand-shake wave before it gives up (s_sleep 2 between: ~1-2 s)
+constexpr unsigned int kHandshakePolls = 1u << 24;
 constexpr int kMbWords = 1024;
 constexpr int kP2pMaxRanks = kMbWords - kMbColl;
 constexpr unsigned int kP2pMagic = 0x53513250u;  // "SQ2P"
@@ -193,6 +195,7 @@ struct sq_ctx {
                                // agrees on it across ranks first (ghost planes come from neighbours)
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0|1 pins it)
     bool diag_no_xwait = false;  // SQ_DIAG_NO_XWAIT: timing diagnostics only (results wrong)
+    bool p2p_kernel_handshake = true;  // P2P: the hand-shake as one wave (SQ_P2P_STREAMOPS=1: stream flag ops)
     bool ef_auto = true;    // the timed pick also tries the other edge_first (unless SQ_EDGE_FIRST pins it)
     int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
     bool rims_b = false;    // ... and their rims run on the exchange stream (block_plan)
@@ -811,10 +814,10 @@ int phi4_block(sq_ctx *c, int g) {
         if (!staged_wait && !p2p) continue;            // P2P: the neighbours always read the staged copy
         if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
         float *stg = s.stage + slot;
-        // two linear copies: one 2-D copy of both ranges ran as a rect-copy kernel
-        // of 23 us against 2 x 6 (profiles/r06/c6/tr_p2p)
-        SQ_HIP(hipMemcpyAsync(stg, src_lo[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
-        SQ_HIP(hipMemcpyAsync(stg + (size_t)G * plane, src_hi[i], gbytes, hipMemcpyDeviceToDevice, s.sB));
+        // both ranges in one two-range copy launch (a 2-D hipMemcpy ran as a
+        // rect-copy kernel of 23 us against 2 x 6 for two linear copies,
+        // profiles/r06/c6/tr_p2p)
+        SQ_HIP(sq::p2p_copy2_launch(stg, src_lo[i], stg + (size_t)G * plane, src_hi[i], (size_t)G * plane, s.sB));
         if (staged_wait) SQ_HIP(hipEventRecord(s.evS, s.sB));
         src_lo[i] = stg;
         src_hi[i] = stg + (size_t)G * plane;
@@ -846,13 +849,20 @@ int phi4_block(sq_ctx *c, int g) {
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
         const unsigned int e = ++c->xchg_seq;
         const size_t n = (size_t)G * plane;
-        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
-        SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
-        SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromDn, e));
-        SQ_HIP(hipMemcpyAsync(p0 - n, c->peers[dn].stage + slot + n, gbytes, hipMemcpyDeviceToDevice, s.sB));
-        SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromUp, e));
-        SQ_HIP(hipMemcpyAsync(p0 + (size_t)s.nz * plane, c->peers[up].stage + slot, gbytes, hipMemcpyDeviceToDevice,
-                              s.sB));
+        if (c->p2p_kernel_handshake) {
+            // one wave: "staged e" to both neighbours, then wait for both of theirs
+            SQ_HIP(sq::p2p_handshake_launch(c->peers[up].mbox + kMbStagedFromDn, c->peers[dn].mbox + kMbStagedFromUp,
+                                            c->mbox + kMbStagedFromDn, c->mbox + kMbStagedFromUp, e,
+                                            kHandshakePolls, c->gate_err, s.sB));
+        } else {  // stream-ordered flag writes and waits (SQ_P2P_STREAMOPS=1)
+            SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
+            SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
+            SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromDn, e));
+            SQ_HIP(wait_seq(s.sB, c->mbox + kMbStagedFromUp, e));
+        }
+        // both neighbours' staged copies, pulled by one launch
+        SQ_HIP(sq::p2p_copy2_launch(p0 - n, c->peers[dn].stage + slot + n, p0 + (size_t)s.nz * plane,
+                                    c->peers[up].stage + slot, n, s.sB));
         SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     } else {  // RCCL: one slab per process; this send/recv order pairs correctly for P = 2 too
@@ -978,8 +988,9 @@ int gate_check(sq_ctx *c, bool read_device) {
         if (e) c->gate_failed = true;
     }
     if (c->gate_failed)
-        return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange (their chunks "
-                               "were not stored; the field is corrupt until it is uploaded or initialised again)");
+        return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange, or a P2P "
+                               "hand-shake gave up waiting for a neighbour (the ghost planes are stale; the field is "
+                               "corrupt until it is uploaded or initialised again)");
     return SQ_OK;
 }
 
@@ -1417,6 +1428,7 @@ int create_phi4(sq_ctx *c) {
         if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
         if (const char *e = getenv("SQ_EDGES_STOPEV")) c->edges_stopev = atoi(e) != 0;
         if (const char *e = getenv("SQ_DIAG_NO_XWAIT")) c->diag_no_xwait = atoi(e) != 0;
+        if (const char *e = getenv("SQ_P2P_STREAMOPS")) c->p2p_kernel_handshake = atoi(e) == 0;
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;

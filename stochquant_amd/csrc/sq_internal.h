@@ -118,7 +118,7 @@ struct Phi4StepArgs {
     const unsigned int *gate;
     unsigned int gate_seq;
     int n_reg, tzc, tlen, tlo0, thi0, ntz;
-    int *gate_err;  // set when a wait gave up (kGateSpinMax)
+    int *gate_err;  // bit 0 set when a wait gave up (kGateSpinMax); bit 1: a P2P hand-shake gave up
 };
 constexpr int kStabSlots = 32;
 
@@ -228,6 +228,14 @@ hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double 
 // Peer-pointer transport (sq_p2p.hip): out[i] = fold over q < nranks of
 // slot q's element i, slot q at slots + q * cap bytes, in rank order.
 enum class P2pRed { kMaxU32, kMaxI32, kMaxU64, kMaxF64, kSumF64 };
+// P2P exchange e's hand-shake as one launch of one wave (sq_p2p.hip): write e
+// into both neighbours' mailbox words, then wait for both of ours to reach e;
+// after `polls` polls it gives up and sets bit 1 of *err
+hipError_t p2p_handshake_launch(unsigned int *up_from_dn, unsigned int *dn_from_up, const unsigned int *from_dn,
+                                const unsigned int *from_up, unsigned int e, unsigned int polls, int *err,
+                                hipStream_t s);
+// d0[0..n) = s0[0..n) and d1[0..n) = s1[0..n) in one launch (sq_p2p.hip)
+hipError_t p2p_copy2_launch(float *d0, const float *s0, float *d1, const float *s1, size_t n, hipStream_t s);
 hipError_t p2p_fold_launch(const unsigned char *slots, int nranks, size_t cap, void *out, size_t n, P2pRed red,
                            hipStream_t s);
 
