@@ -195,6 +195,7 @@ struct sq_ctx {
                                // agrees on it across ranks first (ghost planes come from neighbours)
     bool edge_first = true; // deep-halo blocks: last step's edge planes first (SQ_EDGE_FIRST=0|1 pins it)
     bool diag_no_xwait = false;  // SQ_DIAG_NO_XWAIT: timing diagnostics only (results wrong)
+    bool diag_no_ewait = false;  // SQ_DIAG_NO_EWAIT: no EDGES_DONE event at all (timing only, results wrong)
     bool p2p_kernel_handshake = true;  // P2P: the hand-shake as one wave (SQ_P2P_STREAMOPS=1: stream flag ops)
     bool ef_auto = true;    // the timed pick also tries the other edge_first (unless SQ_EDGE_FIRST pins it)
     int core_pairs = 1;     // deep-halo blocks: fused pairs of the core run ahead of the exchange (0: none)
@@ -792,7 +793,7 @@ int phi4_block(sq_ctx *c, int g) {
     }
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
+        if (!c->diag_no_ewait) SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
         if (c->p.comm == SQ_COMM_LOOPBACK) {  // we write the neighbours' ghosts: wait for them too
             SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evE, 0));
             SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + 1) % ns].evE, 0));
@@ -953,7 +954,8 @@ int phi4_block(sq_ctx *c, int g) {
                 SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));
             } else if (op.kind == SQ_OP_EDGES_DONE) {
                 xchg_live = true;
-                if (!c->stop_used) SQ_HIP(hipEventRecord(s.evE, st));  // else bound to the pair before
+                if (!c->stop_used && !c->diag_no_ewait)
+                    SQ_HIP(hipEventRecord(s.evE, st));  // else bound to the pair before
                 c->stop_used = false;
             } else if (op.kind == SQ_OP_SIGNAL || op.kind == SQ_OP_WAIT) {
                 if (op.lo < 0 || op.lo >= kPlanSlots) return fail(SQ_E_STATE, "block op event slot out of range");
@@ -1428,6 +1430,7 @@ int create_phi4(sq_ctx *c) {
         if (const char *e = getenv("SQ_XCHG_BLOCKS")) c->tb_blocks_xchg = std::max(1, atoi(e));
         if (const char *e = getenv("SQ_EDGES_STOPEV")) c->edges_stopev = atoi(e) != 0;
         if (const char *e = getenv("SQ_DIAG_NO_XWAIT")) c->diag_no_xwait = atoi(e) != 0;
+        if (const char *e = getenv("SQ_DIAG_NO_EWAIT")) c->diag_no_ewait = atoi(e) != 0;
         if (const char *e = getenv("SQ_P2P_STREAMOPS")) c->p2p_kernel_handshake = atoi(e) == 0;
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
