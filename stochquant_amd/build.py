@@ -28,9 +28,10 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 HIPCC = os.path.join(ROCM, "bin", "hipcc")
 ARCH = os.environ.get("SQ_OFFLOAD_ARCH", "gfx950")
 
-DEVICE_SOURCES = ["sq_phi4.hip", "sq_qm1d.hip", "sq_qm1d_gs.hip", "sq_selftest.hip", "sq_p2p.hip", "sq_fields.hip"]
+DEVICE_SOURCES = ["sq_phi4.hip", "sq_phi4_run.hip", "sq_qm1d.hip", "sq_qm1d_gs.hip", "sq_selftest.hip", "sq_p2p.hip", "sq_fields.hip"]
 HOST_SOURCES = ["sq_api.cpp", "sq_io.cpp"]
 HEADERS = ["sq_internal.h", "sq_rng.h", "sq_dpp.h", "sq_glibcf.h"]
+INCLUDES = {"sq_phi4_run.hip": ["sq_phi4.hip"]}  # device sources that include another one
 COMMON = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", "-fno-slp-vectorize", "-Wall",
           "-Wno-unused-function"]
 
@@ -75,7 +76,7 @@ def build(force=False, verbose=False):
         o = os.path.join(OBJ, src + ".o")
         flags = COMMON + [f"--offload-arch={ARCH}", "-x", "hip"]
         stamp = o + ".sha"
-        dig = _digest([s] + hdrs, flags)
+        dig = _digest([s] + [os.path.join(CSRC, d) for d in INCLUDES.get(src, [])] + hdrs, flags)
         if not force and os.path.exists(o) and os.path.exists(stamp) and open(stamp).read() == dig:
             continue
         jobs.append(([HIPCC] + flags + ["-c", s, "-o", o], stamp, dig))

@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -272,6 +273,13 @@ struct sq_ctx {
     // every call that would use the field fails until a new field is uploaded
     // or initialised (gate_check / gate_reset)
     bool gate_failed = false;
+    // single slab (SQ_TB2_RUN=1): a call's pairs as ONE resident launch
+    // (sq_phi4_run.hip); run_flags: one epoch word per block, run_base the
+    // epoch every block has reached (gate_err bit 2: a march wait gave up)
+    bool tb_run = false;
+    unsigned int *run_flags = nullptr;
+    int run_nflags = 0;
+    unsigned int run_base = 0;
     struct {
         bool on;
         int tlo0, thi0, tlen;
@@ -535,11 +543,13 @@ void count_step(sq_ctx *c) {
     for (auto &s : c->slabs) c->perf.site_updates += (long long)s.nz * (long long)plane_floats(c);
 }
 
+constexpr int kRunUnsupported = -1000;  // phi4_tb2_range: a resident march does not apply (internal)
+
 // Steps s and s+1 in one launch (sq_phi4.hip, phi4_tb2_kernel) on the planes
 // [lo, hi) of slab s and, when lo2 < hi2, also [lo2, hi2) (a range of the same
 // length): reads buffer in_buf, writes in_buf ^ 1.
 int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo, int hi, int lo2, int hi2,
-                   int periodic, bool timed) {
+                   int periodic, bool timed, int run_pairs = 0) {
     if (hi <= lo) return SQ_OK;
     const int nr = lo2 < hi2 ? 2 : 1, len = hi - lo;
     if (nr == 2 && hi2 - lo2 != len) return fail(SQ_E_STATE, "two-step launch: ranges of different lengths");
@@ -596,6 +606,36 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
         a.ntz = (a.tlen + a.tzc - 1) / a.tzc;
         c->gate_next.on = false;
     }
+    if (run_pairs > 0) {  // one resident launch of run_pairs pairs (the caller left no frame / stamp / stop state)
+        const int pairs = run_pairs;
+        if (c->profiling == 1 || c->run_flags == nullptr || c->gate_err == nullptr || !sq::phi4_tb2_run_ok(a, c->dev))
+            return kRunUnsupported;  // nothing consumed: the caller falls back to one launch per pair
+        sq::Tb2RunArgs r{c->run_flags, c->gate_err, c->run_base, pairs, nullptr};
+        // diagnostics: SQ_DIAG_RUN_STAMPS=<file> appends each launch's per-pair
+        // block stamps (Tb2RunArgs::stamps) as {npairs, nblocks, words...} u64
+        const char *dpath = getenv("SQ_DIAG_RUN_STAMPS");
+        const size_t nst = 2 * (size_t)pairs * a.nunits + a.nunits;
+        if (dpath) SQ_HIP(hipMalloc(&r.stamps, nst * sizeof(unsigned long long)));
+        uint64_t kid = 0;
+        SQ_HIP(sq::phi4_tb2_run_launch(a, r, st, nullptr, nullptr, &kid));
+        if (dpath) {
+            std::vector<unsigned long long> h(nst + 2);
+            h[0] = (unsigned long long)pairs;
+            h[1] = (unsigned long long)a.nunits;
+            SQ_HIP(hipStreamSynchronize(st));
+            SQ_HIP(hipMemcpy(h.data() + 2, r.stamps, nst * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+            SQ_HIP(hipFree(r.stamps));
+            if (FILE *f = fopen(dpath, "ab")) {
+                fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+                fclose(f);
+            }
+        }
+        c->run_base += (unsigned int)pairs;
+        c->perf.kernel_launches += 1;
+        c->kstat[kid] += 1;
+        c->perf.fused_steps += 2 * pairs;
+        return SQ_OK;
+    }
     EvPair *e = nullptr;
     if (timed && c->profiling == 1) {
         int rc = ev_take(c, &e);
@@ -631,6 +671,17 @@ int phi4_tb2_pair(sq_ctx *c) {
     c->cur ^= 1;
     count_step(c);
     count_step(c);
+    return SQ_OK;
+}
+
+// Single slab, SQ_TB2_RUN=1: `pairs` pairs as one resident launch
+// (sq_phi4_run.hip); the output lands in buffer cur ^ (pairs & 1).
+int phi4_tb2_run_pairs(sq_ctx *c, int pairs) {
+    Slab &s = c->slabs[0];
+    int rc = phi4_tb2_range(c, s, c->cur, s.sA, 0, s.nz, 0, 0, 1, true, pairs);
+    if (rc) return rc;
+    c->cur ^= pairs & 1;
+    for (int i = 0; i < 2 * pairs; ++i) count_step(c);
     return SQ_OK;
 }
 
@@ -990,15 +1041,19 @@ int gate_check(sq_ctx *c, bool read_device) {
         if (e) c->gate_failed = true;
     }
     if (c->gate_failed)
-        return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange, or a P2P "
-                               "hand-shake gave up waiting for a neighbour (the ghost planes are stale; the field is "
-                               "corrupt until it is uploaded or initialised again)");
+        return fail(SQ_E_COMM, "slab exchange: gated rim chunks timed out waiting for the exchange, a P2P "
+                               "hand-shake gave up waiting for a neighbour, or a resident march's block gave up "
+                               "waiting for its neighbours (planes are stale; the field is corrupt until it is "
+                               "uploaded or initialised again)");
     return SQ_OK;
 }
 
 // a new field replaces every plane: the timed-out chunks no longer matter
+// (a resident march's epochs start over too: a timed-out launch left them uneven)
 int gate_reset(sq_ctx *c) {
     if (c->gate_err) SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
+    if (c->run_flags) SQ_HIP(hipMemset(c->run_flags, 0, (size_t)c->run_nflags * sizeof(unsigned int)));
+    c->run_base = 0;
     c->gate_failed = false;
     return SQ_OK;
 }
@@ -1112,6 +1167,25 @@ int phi4_steps(sq_ctx *c, int n) {
 
 int phi4_steps_impl(sq_ctx *c, int n) {
     if (c->p.comm == SQ_COMM_NONE) {
+        if (c->tb_run && c->tbz > 0 && n >= 4 && !c->in_frame && c->snap_next == nullptr &&
+            c->stamps_next == nullptr && c->stop_next == nullptr && c->fold_next.cin == nullptr && !c->clr_armed &&
+            !c->clr_first) {
+            int rc = gate_check(c, false);  // no march on a field a timed-out launch left corrupt
+            if (rc) return rc;
+            // SQ_TB2_RUN_MAXP (experiments): at most this many pairs per launch
+            const char *mp = getenv("SQ_TB2_RUN_MAXP");
+            const int maxp = mp ? std::max(1, atoi(mp)) : INT_MAX;
+            while (n >= 2) {
+                const int np = std::min(n / 2, maxp);
+                rc = phi4_tb2_run_pairs(c, np);
+                if (rc == kRunUnsupported) {
+                    c->tb_run = false;  // this context's shape: one launch per pair from now on
+                    break;
+                }
+                if (rc) return rc;
+                n -= 2 * np;
+            }
+        }
         for (; c->tbz > 0 && n >= 2; n -= 2) {
             int rc = phi4_tb2_pair(c);
             if (rc) return rc;
@@ -1432,6 +1506,18 @@ int create_phi4(sq_ctx *c) {
         if (const char *e = getenv("SQ_DIAG_NO_XWAIT")) c->diag_no_xwait = atoi(e) != 0;
         if (const char *e = getenv("SQ_DIAG_NO_EWAIT")) c->diag_no_ewait = atoi(e) != 0;
         if (const char *e = getenv("SQ_P2P_STREAMOPS")) c->p2p_kernel_handshake = atoi(e) == 0;
+        const char *rn = getenv("SQ_TB2_RUN");
+        if (rn && atoi(rn) != 0 && p.comm == SQ_COMM_NONE && c->slabs.size() == 1) {
+            // one epoch word per block: at most Ly / 8 y-bands x nz / 2 chunks (>= 2 planes each)
+            c->run_nflags = (c->Ly / 8) * std::max(1, c->slabs[0].nz / 2);
+            SQ_HIP(hipMalloc(&c->run_flags, (size_t)c->run_nflags * sizeof(unsigned int)));
+            SQ_HIP(hipMemset(c->run_flags, 0, (size_t)c->run_nflags * sizeof(unsigned int)));
+            if (c->gate_err == nullptr) {
+                SQ_HIP(hipMalloc(&c->gate_err, sizeof(int)));
+                SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
+            }
+            c->tb_run = true;
+        }
     }
     SQ_HIP(hipDeviceSynchronize());  // the set-up memsets ran on the null stream
     return SQ_OK;
@@ -2195,6 +2281,7 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->coll);
     (void)hipFree(c->gate_word);
     (void)hipFree(c->gate_err);
+    (void)hipFree(c->run_flags);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &s : c->slabs) {
         (void)hipFree(s.buf[0]);
@@ -2819,7 +2906,12 @@ int sq_phi4_launch_info(sq_ctx *c, char *name, size_t cap, long long *grid_threa
             best = kv.first;
             n = kv.second;
         }
-    if (n > 0) sq::phi4_kernel_id_name(best, name, cap);
+    if (n > 0) {
+        if ((best & 3) == 3)
+            sq::phi4_run_kernel_id_name(best, name, cap);
+        else
+            sq::phi4_kernel_id_name(best, name, cap);
+    }
     if (grid_threads) *grid_threads = n > 0 ? (long long)sq::phi4_kernel_id_grid(best) : 0;
     if (launches) *launches = n;
     return SQ_OK;

@@ -192,11 +192,35 @@ bool phi4_tb2_supported(int Lx, int Ly);
 hipError_t phi4_tb2_launch(const Phi4StepArgs &a, hipStream_t s, hipEvent_t start = nullptr,
                            hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
 
+// Several two-step pairs in ONE resident launch (sq_phi4_run.hip): pair t reads
+// a.in (t even) or a.out (t odd) and writes the other, steps s + 2t and s + 2t + 1;
+// a block starts pair t + 1 once its 3 x 3 neighbourhood of blocks (y-bands x
+// z-chunks, periodic) has finished pair t.  flags: one word per block, the epoch
+// base + t + 1 after pair t (base: the context's running count, so nothing is
+// cleared between launches); err: bit 2 set when a wait gave up (kRunSpinMax),
+// which ends every block's waits.  Single periodic slab of 256-site rows, no
+// frames, every block resident (phi4_tb2_run_ok).
+struct Tb2RunArgs {
+    unsigned int *flags;
+    int *err;
+    unsigned int base;
+    int npairs;
+    // diagnostics (nullable, SQ_DIAG_RUN_STAMPS): per pair t and block b, the
+    // constant 100 MHz clock at [2 (t nb + b)] the pair's start (its wait done)
+    // and [+1] its end (stores drained); then per block its hardware slot
+    // (XCC_ID << 16 | HW_ID) at [2 npairs nb + b]
+    unsigned long long *stamps;
+};
+bool phi4_tb2_run_ok(const Phi4StepArgs &a, int dev);
+hipError_t phi4_tb2_run_launch(const Phi4StepArgs &a, const Tb2RunArgs &r, hipStream_t s, hipEvent_t start = nullptr,
+                               hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
+void phi4_run_kernel_id_name(uint64_t kid, char *name, size_t cap);
+
 // Kernel identity of a launch (kid out-parameters of the launchers): the
 // template instance the launcher picked, packed with the grid in threads (high
 // 32 bits), so a caller can name the dominant kernel exactly as rocprofv3 does
 // (sq_phi4_launch_info; bench.py ties its committed PMC record to it).
-void phi4_kernel_id_name(uint64_t kid, char *name, size_t cap);
+void phi4_kernel_id_name(uint64_t kid, char *name, size_t cap);  // family 3: phi4_run_kernel_id_name
 inline unsigned phi4_kernel_id_grid(uint64_t kid) { return (unsigned)(kid >> 32); }
 
 // Picks the register tile for (Lx, Ly); returns false if unsupported.

@@ -1058,7 +1058,7 @@ __device__ __forceinline__ void tb_wait_nbrs(const int *prog, int w, int need) {
     }
 }
 
-template <bool NZ, bool WIDE, bool FR, bool WH, int J, bool P2 = false>
+template <bool NZ, bool WIDE, bool FR, bool WH, int J, bool P2 = false, int LAUX = 0>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, TbRun &R, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
@@ -1078,9 +1078,9 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         rc = plane_rsrc(A.in, tb_pidx(A, p), K.plane, K.pbytes);
     }
     if (!WIDE || K.w < kTbWaves) {
-        I2.row = bload4(rs, K.voff, ss);
-        I2.hm = bload4(rs, K.vm, ss);
-        I2.hp = bload4(rs, K.vp, ss);
+        I2.row = bload4<LAUX>(rs, K.voff, ss);
+        I2.hm = bload4<LAUX>(rs, K.vm, ss);
+        I2.hp = bload4<LAUX>(rs, K.vp, ss);
         float ex = 0.f;
         if constexpr (WIDE) ex = bload1(rc, K.vex, sc);
         const f32x4n xa = tb_noise<NZ>(A, R.qz, K.qoff, K.slo, K.shi);
@@ -1853,6 +1853,7 @@ __global__ __launch_bounds__(256) void phi4_slices_kernel(const float *slab, lon
 
 }  // namespace
 
+#ifndef SQ_PHI4_KERNELS_ONLY  // sq_phi4_run.hip includes the kernels above, not the launchers below
 bool phi4_geometry(int Lx, int Ly, Phi4Geom *g) {
     if (Lx <= 0 || Ly <= 0 || (Lx & 3)) return false;
     int qx;
@@ -2110,4 +2111,5 @@ hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double 
     return hipGetLastError();
 }
 
+#endif  // SQ_PHI4_KERNELS_ONLY
 }  // namespace sq
