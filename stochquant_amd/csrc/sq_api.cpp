@@ -276,6 +276,18 @@ struct sq_ctx {
     // single slab (SQ_TB2_RUN=1): a call's pairs as ONE resident launch
     // (sq_phi4_run.hip); run_flags: one epoch word per block, run_base the
     // epoch every block has reached (gate_err bit 2: a march wait gave up)
+    // P2P, SQ_P2P_KSTAGE=1: the last pair of a deep-halo block writes the next
+    // exchange's staging slot itself and counts its blocks into kstage_ctr
+    // (phi4_tb2_stage_kernel); the exchange's hand-shake waits for kstage_n
+    // instead of the EDGES_DONE event plus a staging copy.  kstage_pending:
+    // the slot holds the current field's edges (dropped when anything else
+    // writes the field); evE_stale: EDGES_DONE was not recorded behind that
+    // pair, so an exchange of the old form records it first
+    bool p2p_kstage = false;
+    unsigned int *kstage_ctr = nullptr;
+    unsigned int kstage_n = 0;
+    bool kstage_pending = false, kstage_next = false, kstage_issued = false, evE_stale = false;
+    float *kstage_slot = nullptr;
     bool tb_run = false;
     unsigned int *run_flags = nullptr;
     int run_nflags = 0;
@@ -650,7 +662,12 @@ int phi4_tb2_range(sq_ctx *c, const Slab &s, int in_buf, hipStream_t st, int lo,
     hipEvent_t stop = c->stop_next;
     c->stop_next = nullptr;
     uint64_t kid = 0;
-    if (e == nullptr && stop != nullptr) {
+    if (c->kstage_next && stop == nullptr && sq::phi4_tb2_stage_ok(a, c->gz)) {
+        const sq::Tb2StageArgs g{c->kstage_slot, c->gz, c->kstage_ctr};
+        SQ_HIP(sq::phi4_tb2_stage_launch(a, g, st, e ? e->a : nullptr, e ? e->b : nullptr, &kid));
+        c->kstage_n += (unsigned int)a.nunits;
+        c->kstage_issued = true;
+    } else if (e == nullptr && stop != nullptr) {
         SQ_HIP(sq::phi4_tb2_launch(a, st, nullptr, stop, &kid));
         c->stop_used = true;
     } else {
@@ -842,8 +859,18 @@ int phi4_block(sq_ctx *c, int g) {
         src_lo[i] = p0;
         src_hi[i] = p0 + (size_t)(s.nz - G) * plane;
     }
+    // P2P with the staging slot already written by the previous block's last
+    // pair (kstage): no EDGES_DONE wait and no staging copy on stream B, the
+    // hand-shake waits for that pair's block count instead
+    const bool kst = c->p.comm == SQ_COMM_P2P && c->kstage_pending && ns == 1 && c->p2p_kernel_handshake;
+    c->kstage_pending = false;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
+        if (kst) continue;
+        if (c->evE_stale) {  // the last pair before is complete in stream-A order: record it now
+            SQ_HIP(hipEventRecord(s.evE, s.sA));
+            c->evE_stale = false;
+        }
         if (!c->diag_no_ewait) SQ_HIP(hipStreamWaitEvent(s.sB, s.evE, 0));
         if (c->p.comm == SQ_COMM_LOOPBACK) {  // we write the neighbours' ghosts: wait for them too
             SQ_HIP(hipStreamWaitEvent(s.sB, c->slabs[(i + ns - 1) % ns].evE, 0));
@@ -863,6 +890,7 @@ int phi4_block(sq_ctx *c, int g) {
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
         const bool staged_wait = plans[i][0].lo == 1;  // core pair 1 waits for the copy (WAIT_STAGED)
+        if (kst) continue;                              // the slot is written already
         if (!staged_wait && !p2p) continue;            // P2P: the neighbours always read the staged copy
         if (!s.stage) return fail(SQ_E_STATE, "staged exchange without a staging buffer");
         float *stg = s.stage + slot;
@@ -905,7 +933,8 @@ int phi4_block(sq_ctx *c, int g) {
             // one wave: "staged e" to both neighbours, then wait for both of theirs
             SQ_HIP(sq::p2p_handshake_launch(c->peers[up].mbox + kMbStagedFromDn, c->peers[dn].mbox + kMbStagedFromUp,
                                             c->mbox + kMbStagedFromDn, c->mbox + kMbStagedFromUp, e,
-                                            kHandshakePolls, c->gate_err, s.sB));
+                                            kHandshakePolls, c->gate_err, s.sB, kst ? c->kstage_ctr : nullptr,
+                                            c->kstage_n));
         } else {  // stream-ordered flag writes and waits (SQ_P2P_STREAMOPS=1)
             SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
             SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
@@ -986,12 +1015,21 @@ int phi4_block(sq_ctx *c, int g) {
                 if (c->edges_stopev && op.kind == SQ_OP_PAIR && oi + 1 < ops.size() &&
                     ops[oi + 1].kind == SQ_OP_EDGES_DONE && ops[oi + 1].stream == op.stream)
                     c->stop_next = s.evE;  // phi4_tb2_range binds it to the launch (stop_used)
+                // P2P kstage: the block's last pair (the whole slab, right before
+                // EDGES_DONE) also writes the next exchange's staging slot
+                c->kstage_issued = false;
+                c->kstage_next = p2p && c->p2p_kstage && ns == 1 && c->p2p_kernel_handshake && !c->in_frame &&
+                                 s.stage != nullptr && op.kind == SQ_OP_PAIR && op.stream == kA && op.lo == 0 &&
+                                 op.hi == s.nz && op.lo2 >= op.hi2 && oi + 1 < ops.size() &&
+                                 ops[oi + 1].kind == SQ_OP_EDGES_DONE && ops[oi + 1].stream == kA;
+                if (c->kstage_next) c->kstage_slot = s.stage + (size_t)((c->xchg_seq + 1) & 1u) * slot_stride;
                 if (op.kind == SQ_OP_PAIR)
                     rc = phi4_tb2_range(c, s, in, st, op.lo, op.hi, op.lo2, op.hi2, 0, first);
                 else if (op.lo2 < op.hi2)  // two equal ranges in one launch: two chunks zstep apart
                     rc = phi4_launch_range(c, s, in, st, op.lo, op.hi2, op.lo2 - op.lo, op.hi - op.lo, 2, 0, first);
                 else
                     rc = phi4_launch_span(c, s, in, st, op.lo, op.hi, first);
+                c->kstage_next = false;
                 c->stop_next = nullptr;  // an empty range launched nothing: EDGES_DONE records
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
                 if (op.stream != kB) xchg_live = false;
@@ -1002,11 +1040,17 @@ int phi4_block(sq_ctx *c, int g) {
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + 1) % ns].evC, 0));
                 }
             } else if (op.kind == SQ_OP_WAIT_STAGED) {
-                SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));
+                if (!kst) SQ_HIP(hipStreamWaitEvent(st, s.evS, 0));  // kstage: no copy reads the field
             } else if (op.kind == SQ_OP_EDGES_DONE) {
                 xchg_live = true;
-                if (!c->stop_used && !c->diag_no_ewait)
+                if (c->kstage_issued) {  // the next exchange waits for the pair's block count instead
+                    c->kstage_pending = true;
+                    c->evE_stale = true;
+                    c->kstage_issued = false;
+                } else if (!c->stop_used && !c->diag_no_ewait) {
                     SQ_HIP(hipEventRecord(s.evE, st));  // else bound to the pair before
+                    c->evE_stale = false;
+                }
                 c->stop_used = false;
             } else if (op.kind == SQ_OP_SIGNAL || op.kind == SQ_OP_WAIT) {
                 if (op.lo < 0 || op.lo >= kPlanSlots) return fail(SQ_E_STATE, "block op event slot out of range");
@@ -1053,6 +1097,7 @@ int gate_check(sq_ctx *c, bool read_device) {
 int gate_reset(sq_ctx *c) {
     if (c->gate_err) SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
     if (c->run_flags) SQ_HIP(hipMemset(c->run_flags, 0, (size_t)c->run_nflags * sizeof(unsigned int)));
+    c->kstage_pending = false;  // the staged edges are the old field's
     c->run_base = 0;
     c->gate_failed = false;
     return SQ_OK;
@@ -1417,6 +1462,13 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipMemset(c->gate_err, 0, sizeof(int)));
         const char *e = getenv("SQ_SLAB_GATE");
         c->slab_gate = e ? atoi(e) != 0 : false;  // off: its spinning rim blocks hold the CU slots the exchange needs
+    }
+    if (p.comm == SQ_COMM_P2P) {
+        // the last pair's block count (phi4_tb2_stage_kernel; monotonic, never reset)
+        SQ_HIP(hipMalloc(&c->kstage_ctr, 64));
+        SQ_HIP(hipMemset(c->kstage_ctr, 0, 64));
+        const char *ks = getenv("SQ_P2P_KSTAGE");
+        c->p2p_kstage = ks ? atoi(ks) != 0 : false;
     }
     if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
         // fine-grained device memory: the words are written by the peers'
@@ -1879,6 +1931,7 @@ int phi4_frame(sq_ctx *c, int *stable) {
     rc = one_stream ? SQ_OK : phi4_join(c);
     if (rc) return rc;
     c->in_frame = true;
+    c->kstage_pending = false;  // frames stage their exchanges by copy
     c->frame_step0 = c->step;
     // the agreed value: a rollback restores it on every rank alike (an
     // unagreed local value would let a rank with fin = 1 take the guard's fast
@@ -2068,6 +2121,7 @@ int phi4_frames_dev(sq_ctx *c, int n, int *stable, double *dtau_out) {
         else
             SQ_HIP(hipMemcpyAsync(s0.snap, plane0(c, s0, c->cur), nfl * sizeof(float), hipMemcpyDeviceToDevice, st));
         c->in_frame = true;
+        c->kstage_pending = false;  // frames stage their exchanges by copy
         c->dev_frames = true;
         c->ctl_cur = c->ctl + (i & 1);
         c->frame_step0 = c->step;
@@ -2282,6 +2336,7 @@ int sq_destroy(sq_ctx *c) {
     (void)hipFree(c->gate_word);
     (void)hipFree(c->gate_err);
     (void)hipFree(c->run_flags);
+    (void)hipFree(c->kstage_ctr);
     if (c->comm) (void)ncclCommDestroy(c->comm);
     for (auto &s : c->slabs) {
         (void)hipFree(s.buf[0]);

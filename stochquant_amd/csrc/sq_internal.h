@@ -216,6 +216,22 @@ hipError_t phi4_tb2_run_launch(const Phi4StepArgs &a, const Tb2RunArgs &r, hipSt
                                hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
 void phi4_run_kernel_id_name(uint64_t kid, char *name, size_t cap);
 
+// The last pair of a P2P deep-halo block with its edge planes also stored into
+// the next exchange's staging slot (sq_phi4_run.hip): phi4_tb2_kernel's
+// launch (one range, 256-site rows, no frame records) whose output planes
+// [0, G) and [nz - G, nz) are also written, write-through, to stage[0, G)
+// and stage[G, 2G) planes; every block then adds 1 to *ctr behind its drained
+// stores, so the exchange stream's hand-shake waits for the count
+// (p2p_handshake_launch's pre) instead of a cross-stream event and a copy.
+struct Tb2StageArgs {
+    float *stage;
+    int G;
+    unsigned int *ctr;
+};
+bool phi4_tb2_stage_ok(const Phi4StepArgs &a, int G);
+hipError_t phi4_tb2_stage_launch(const Phi4StepArgs &a, const Tb2StageArgs &g, hipStream_t s,
+                                 hipEvent_t start = nullptr, hipEvent_t stop = nullptr, uint64_t *kid = nullptr);
+
 // Kernel identity of a launch (kid out-parameters of the launchers): the
 // template instance the launcher picked, packed with the grid in threads (high
 // 32 bits), so a caller can name the dominant kernel exactly as rocprofv3 does
@@ -254,10 +270,11 @@ hipError_t phi4_slices_launch(const float *slab, int Lx, int Ly, int nz, double 
 enum class P2pRed { kMaxU32, kMaxI32, kMaxU64, kMaxF64, kSumF64 };
 // P2P exchange e's hand-shake as one launch of one wave (sq_p2p.hip): write e
 // into both neighbours' mailbox words, then wait for both of ours to reach e;
-// after `polls` polls it gives up and sets bit 1 of *err
+// after `polls` polls it gives up and sets bit 1 of *err.  pre (nullable):
+// first wait until *pre has reached pre_n (phi4_tb2_stage_launch's count)
 hipError_t p2p_handshake_launch(unsigned int *up_from_dn, unsigned int *dn_from_up, const unsigned int *from_dn,
                                 const unsigned int *from_up, unsigned int e, unsigned int polls, int *err,
-                                hipStream_t s);
+                                hipStream_t s, const unsigned int *pre = nullptr, unsigned int pre_n = 0);
 // d0[0..n) = s0[0..n) and d1[0..n) = s1[0..n) in one launch (sq_p2p.hip)
 hipError_t p2p_copy2_launch(float *d0, const float *s0, float *d1, const float *s1, size_t n, hipStream_t s);
 hipError_t p2p_fold_launch(const unsigned char *slots, int nranks, size_t cap, void *out, size_t n, P2pRed red,

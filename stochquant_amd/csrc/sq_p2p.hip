@@ -73,8 +73,22 @@ __global__ void __launch_bounds__(256) p2p_copy2_kernel(float *__restrict__ d0, 
 // follows then copies whatever is there, and the field is void.
 __global__ void __launch_bounds__(64) p2p_handshake_kernel(unsigned int *up_from_dn, unsigned int *dn_from_up,
                                                           const unsigned int *from_dn, const unsigned int *from_up,
-                                                          unsigned int e, unsigned int polls, int *err) {
+                                                          unsigned int e, unsigned int polls, int *err,
+                                                          const unsigned int *pre, unsigned int pre_n) {
     if (threadIdx.x != 0) return;
+    // pre: the staging slot is written by the block's last pair on the
+    // interior stream (phi4_tb2_stage_kernel, write-through stores drained
+    // before each block's count): wait until all its blocks have counted
+    if (pre != nullptr) {
+        for (unsigned int k = 0;; ++k) {
+            if ((int)(__hip_atomic_load(pre, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - pre_n) >= 0) break;
+            if (k >= polls) {
+                if (err) __hip_atomic_fetch_or(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
     __threadfence_system();
     __hip_atomic_store(up_from_dn, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(dn_from_up, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -94,8 +108,8 @@ __global__ void __launch_bounds__(64) p2p_handshake_kernel(unsigned int *up_from
 
 hipError_t p2p_handshake_launch(unsigned int *up_from_dn, unsigned int *dn_from_up, const unsigned int *from_dn,
                                 const unsigned int *from_up, unsigned int e, unsigned int polls, int *err,
-                                hipStream_t s) {
-    p2p_handshake_kernel<<<1, 64, 0, s>>>(up_from_dn, dn_from_up, from_dn, from_up, e, polls, err);
+                                hipStream_t s, const unsigned int *pre, unsigned int pre_n) {
+    p2p_handshake_kernel<<<1, 64, 0, s>>>(up_from_dn, dn_from_up, from_dn, from_up, e, polls, err, pre, pre_n);
     return hipGetLastError();
 }
 

@@ -1011,6 +1011,11 @@ struct TbCtx {
     int z0, z1, w, lane;
     bool outw;
     int snapw;  // FR: an output row wave of a launch that stores the frame's snapshot
+    // STG (sq_phi4_run.hip, phi4_tb2_stage_kernel): the P2P staging slot, whose
+    // first stg_g planes take output planes [0, stg_g) and next stg_g planes
+    // output planes [stg_hi, stg_hi + stg_g)
+    __amdgpu_buffer_rsrc_t rstg;
+    int stg_g, stg_hi;
 };
 
 // Wave-uniform per-plane scalars carried through the march instead of being
@@ -1058,7 +1063,7 @@ __device__ __forceinline__ void tb_wait_nbrs(const int *prog, int w, int need) {
     }
 }
 
-template <bool NZ, bool WIDE, bool FR, bool WH, int J, bool P2 = false, int LAUX = 0>
+template <bool NZ, bool WIDE, bool FR, bool WH, int J, bool P2 = false, int LAUX = 0, bool STG = false>
 __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, TbRun &R, int p, const TbIn &I0,
                                          const TbIn &I1, TbIn &I2, const float4 &T0, const float4 &T1, float4 &T2,
                                          float4 (*lds)[kTbWaves][64], float (*tx)[kTbWaves][2], FrameAcc &f1,
@@ -1143,6 +1148,11 @@ __device__ __forceinline__ void tb_plane(const Phi4StepArgs &A, const TbCtx &K, 
         if constexpr (WH) {
             // the plane offset in the VGPR offset, soffset 0: see bstore4
             bstore4<17>(K.rout, K.voff + (uint32_t)(p - 1 + A.gz) * K.pbytes, o);
+            if constexpr (STG) {  // an edge plane: also into the staging slot (write-through, as the field)
+                const int q = p - 1;
+                if (q < K.stg_g) bstore4<17>(K.rstg, K.voff + (uint32_t)q * K.pbytes, o);
+                if (q >= K.stg_hi) bstore4<17>(K.rstg, K.voff + (uint32_t)(q - K.stg_hi + K.stg_g) * K.pbytes, o);
+            }
         } else {
             const __amdgpu_buffer_rsrc_t ws = plane_rsrc(A.out, p - 1 + A.gz, K.plane, K.pbytes);
             bstore4<17>(ws, K.voff, o);

@@ -180,11 +180,125 @@ void phi4_tb2_run_kernel(const Phi4StepArgs A0, const Tb2RunArgs R0) {
     }
 }
 
+// phi4_tb2_kernel<NZ, false, 1, false, true, false> for the last pair of a
+// P2P deep-halo block (one range of a slab with ghost zones): its edge output
+// planes also go to the staging slot, and every block counts itself done.
+template <bool NZ>
+__global__ __launch_bounds__(kTbWaves * 64) __attribute__((amdgpu_waves_per_eu(1)))
+void phi4_tb2_stage_kernel(const Phi4StepArgs A, const Tb2StageArgs S) {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const TbBlock tbk = tb_block<false>(A, b, nb);
+    const int Lx = A.Lx, Ly = A.Ly;
+    TbCtx K;
+    K.w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    K.lane = threadIdx.x & 63;
+    K.outw = K.w >= 1 && K.w <= kTbRows;
+    K.z0 = tbk.z0;
+    K.z1 = tbk.z1;
+    K.snapw = 0;
+    K.plane = (size_t)Lx * (size_t)Ly;
+    K.pbytes = (uint32_t)(K.plane * sizeof(float));
+    K.qplane = (uint32_t)(K.plane >> 2);
+    const int nbytes = (int)((uint32_t)(A.nz + 2 * A.gz) * K.pbytes);  // < 2^31 (phi4_tb2_stage_ok)
+    K.rin = __builtin_amdgcn_make_buffer_rsrc((void *)A.in, (short)0, nbytes, 0x00020000);
+    K.rout = __builtin_amdgcn_make_buffer_rsrc((void *)A.out, (short)0, nbytes, 0x00020000);
+    K.rstg = __builtin_amdgcn_make_buffer_rsrc((void *)S.stage, (short)0, (int)(2u * (uint32_t)S.G * K.pbytes),
+                                               0x00020000);
+    K.stg_g = S.G;
+    K.stg_hi = A.nz - S.G;
+    K.qwrap = (uint32_t)A.Lzg * K.qplane;
+    K.m2v = f32x2{A.m2, A.m2};
+    asm volatile("" : "+v"(K.m2v));
+    K.swrap_at = INT_MIN;  // a slab: p < 0 in ghost zones
+    const unsigned long long s0 = ((unsigned long long)A.s_hi << 32) | A.s_lo, s1 = s0 + 1;
+    K.slo = (uint32_t)s0;
+    K.shi = (uint32_t)(s0 >> 32);
+    K.slo1 = (uint32_t)s1;
+    K.shi1 = (uint32_t)(s1 >> 32);
+    {
+        auto wrapy = [Ly](int y) { return y < 0 ? y + Ly : (y >= Ly ? y - Ly : y); };
+        const int y = wrapy(tbk.yb * kTbRows - 1 + K.w);
+        const int ym = wrapy(y - 1), yp = wrapy(y + 1);
+        K.voff = (uint32_t)((y * Lx + 4 * K.lane) * 4);
+        K.vm = (uint32_t)((ym * Lx + 4 * K.lane) * 4);
+        K.vp = (uint32_t)((yp * Lx + 4 * K.lane) * 4);
+        K.vex = 0;
+        K.vx2 = 0;
+        K.qoff = (uint32_t)((y * Lx + 4 * K.lane) >> 2);
+    }
+    __shared__ float4 lds[3][kTbWaves][64];
+    __shared__ float tx[1][kTbWaves][2];
+    TbIn I0, I1, I2;
+    {
+        const __amdgpu_buffer_rsrc_t r0 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 2), K.plane, K.pbytes);
+        const __amdgpu_buffer_rsrc_t r1 = plane_rsrc(A.in, tb_pidx(A, K.z0 - 1), K.plane, K.pbytes);
+        I0.row = bload4(r0, K.voff);
+        I0.hm = I0.hp = I0.row;
+        I1.row = bload4(r1, K.voff);
+        I1.hm = bload4(r1, K.vm);
+        I1.hp = bload4(r1, K.vp);
+    }
+    float4 T0 = make_float4(0.f, 0.f, 0.f, 0.f), T1 = T0, T2 = T0;
+    FrameAcc f1 = frame_acc(), f2 = frame_acc();  // unused (no records)
+    TbRun R;
+    R.scur = (uint32_t)tb_pidx(A, K.z0 - 1) * K.pbytes;
+    R.snext = (uint32_t)tb_pidx(A, K.z0) * K.pbytes;
+    R.qz = (uint32_t)global_z(A, K.z0 - 1) * K.qplane;
+    R.qzm = 0;
+    const int z1 = K.z1;
+    const PrioQ pq(K.z0, z1 - K.z0 + 2);
+    for (int p = K.z0 - 1; p <= z1; p += 3) {
+        if (A.prio) prio_by_progress(pq.q(p));
+        tb_plane<NZ, false, false, true, 0, false, 0, true>(A, K, R, p, I0, I1, I2, T0, T1, T2, lds, tx, f1, f2,
+                                                            nullptr);
+        if (p + 1 > z1) break;
+        tb_plane<NZ, false, false, true, 1, false, 0, true>(A, K, R, p + 1, I1, I2, I0, T1, T2, T0, lds, tx, f1, f2,
+                                                            nullptr);
+        if (p + 2 > z1) break;
+        tb_plane<NZ, false, false, true, 2, false, 0, true>(A, K, R, p + 2, I2, I0, I1, T2, T0, T1, lds, tx, f1, f2,
+                                                            nullptr);
+    }
+    // every wave's write-through stores drained, then one count for the block
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(S.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
-// kid family 3 (phi4_kernel_id_name's bits 0-1): bit 2 NZ, bit 3 LAUX = 16
+// kid family 3 (phi4_kernel_id_name's bits 0-1): bit 2 NZ, bit 3 LAUX = 16,
+// bit 4 the staging kernel
 void phi4_run_kernel_id_name(uint64_t k, char *name, size_t cap) {
-    snprintf(name, cap, "phi4_tb2_run_kernel<%s, %d>", ((k >> 2) & 1) ? "true" : "false", ((k >> 3) & 1) ? 16 : 0);
+    if ((k >> 4) & 1)
+        snprintf(name, cap, "phi4_tb2_stage_kernel<%s>", ((k >> 2) & 1) ? "true" : "false");
+    else
+        snprintf(name, cap, "phi4_tb2_run_kernel<%s, %d>", ((k >> 2) & 1) ? "true" : "false",
+                 ((k >> 3) & 1) ? 16 : 0);
+}
+
+bool phi4_tb2_stage_ok(const Phi4StepArgs &a, int G) {
+    return a.Lx == 256 && a.Ly % kTbRows == 0 && !a.periodic && a.nxseg == 1 && a.nyg == a.Ly / kTbRows &&
+           a.nzr == a.nzc && a.nunits == a.nyg * a.nzc && a.zlo == 0 && a.zlen == a.nz && a.nz >= 2 &&
+           (long long)a.zc * a.nzr >= a.zlen && G >= 1 && G <= a.nz && a.gz >= 2 && a.gate == nullptr &&
+           a.flag == nullptr && a.st_md == nullptr && a.snap == nullptr && a.dcoef == nullptr &&
+           a.stamps == nullptr && a.tctl == nullptr && a.fold.cin == nullptr && a.clr.md == nullptr &&
+           (long long)(a.nz + 2 * a.gz) * a.Lx * a.Ly * 4 < (1ll << 31);
+}
+
+hipError_t phi4_tb2_stage_launch(const Phi4StepArgs &a, const Tb2StageArgs &g, hipStream_t s, hipEvent_t e0,
+                                 hipEvent_t e1, uint64_t *kid) {
+    if (!phi4_tb2_stage_ok(a, g.G) || g.stage == nullptr || g.ctr == nullptr) return hipErrorInvalidValue;
+    const bool nz = a.sig != 0.0f;
+    const dim3 grid((unsigned)a.nunits), block(kTbWaves * 64);
+    if (kid != nullptr) *kid = (uint64_t)3 | (uint64_t)nz << 2 | (uint64_t)1 << 4 | (uint64_t)(grid.x * block.x) << 32;
+    Phi4StepArgs q = a;
+    static const int prio = getenv("SQ_TB2_PRIO") ? atoi(getenv("SQ_TB2_PRIO")) : 1;
+    q.prio = prio;
+    Tb2StageArgs gg = g;
+    void *args[] = {&q, &gg};
+    const void *fn = nz ? (const void *)&phi4_tb2_stage_kernel<true> : (const void *)&phi4_tb2_stage_kernel<false>;
+    if (e0 != nullptr || e1 != nullptr) return hipExtLaunchKernel(fn, grid, block, args, 0, s, e0, e1, 0);
+    return hipLaunchKernel(fn, grid, block, args, 0, s);
 }
 
 static int run_laux() {

@@ -118,6 +118,36 @@ def test_p2p_single_rank_in_process(gpu):
         assert np.array_equal(L.download(), mono["field"][0])
 
 
+@pytest.mark.parametrize("ghost", ["4", "16"])
+def test_p2p_single_rank_kernel_staged(gpu, monkeypatch, ghost):
+    """P = 1 with SQ_P2P_KSTAGE=1: several step calls (each block's last pair
+    stages the next exchange, across calls too), an upload in between (the
+    staged edges are dropped and re-staged by copy), a frame (frames stage by
+    copy) and more steps: bit-identical to the single periodic slab."""
+    shape = (256, 16, 48)
+    phi0, phi1 = _field0(shape), _field0(shape, seed=3)
+    kw = dict(KW, loops=6)
+    script = [("upload", phi0), ("step", 20), ("step", 13), ("field", None), ("upload", phi1), ("step", 9),
+              ("frame", None), ("step", 24), ("field", None)]
+    mono = _mono(shape, kw, script)
+    monkeypatch.setenv("SQ_P2P_KSTAGE", "1")
+    monkeypatch.setenv("SQ_GHOST", ghost)
+    got = []
+    with _lat(shape, comm="p2p", nranks=1, rank=0, **kw) as L:
+        L.p2p_connect([L.p2p_handle()])
+        for op, arg in script:
+            if op == "upload":
+                L.upload(arg)
+            elif op == "step":
+                L.step(arg)
+            elif op == "frame":
+                assert bool(L.run_frame()) == mono["stable"][0]
+            elif op == "field":
+                got.append(L.download())
+    for a, b in zip(got, mono["field"]):
+        assert np.array_equal(a, b)
+
+
 def test_p2p_unconnected_context_refuses_to_step(gpu):
     from stochquant_amd import StochQuantError
     with _lat((64, 16, 24), comm="p2p", nranks=2, rank=0, **KW) as L:
@@ -140,6 +170,13 @@ def test_p2p_unconnected_context_refuses_to_step(gpu):
     # slab's two peers distinct ranks, fused pairs and core pairs
     (8, (64, 8, 64), 17, {"SQ_GHOST": "4"}),
     (8, (256, 16, 256), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2"}),
+    # the last pair of each block writes the next exchange's staging slot and
+    # counts its blocks (SQ_P2P_KSTAGE=1, phi4_tb2_stage_kernel)
+    (2, (256, 16, 64), 21, {"SQ_GHOST": "8", "SQ_P2P_KSTAGE": "1"}),
+    (3, (256, 16, 96), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2", "SQ_P2P_KSTAGE": "1"}),
+    (2, (256, 16, 64), 30, {"SQ_GHOST": "16", "SQ_CORE_PAIRS": "0", "SQ_P2P_KSTAGE": "1"}),
+    (8, (256, 16, 256), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2", "SQ_P2P_KSTAGE": "1"}),
+    (4, (256, 8, 20), 33, {"SQ_GHOST": "4", "SQ_P2P_KSTAGE": "1"}),  # slabs of 5 planes: edges overlap
 ])
 def test_p2p_ranks_bitwise_vs_single_slab(gpu, nranks, shape, steps, env):
     phi0 = _field0(shape)
@@ -217,6 +254,12 @@ def test_p2p_frames_with_noise(gpu):
     script = [("upload", phi0), ("frame", None), ("step", 7), ("frame", None), ("field", None)]
     mono = _mono(shape, kw, script)
     outs = run_ranks(2, shape, kw, script, {"SQ_GHOST": "4"})
+    for o in outs:
+        assert o["stable"] == mono["stable"] == [True, True]
+        assert o["TV"] == mono["TV"]
+    assert np.array_equal(_assemble(outs), mono["field"][0])
+    # the same with the kernel-staged exchange between the frames
+    outs = run_ranks(2, shape, kw, script, {"SQ_GHOST": "4", "SQ_P2P_KSTAGE": "1"})
     for o in outs:
         assert o["stable"] == mono["stable"] == [True, True]
         assert o["TV"] == mono["TV"]
