@@ -382,8 +382,9 @@ def measure(a, lat, world, slab_path, watch=None):
         phase("trial_blocks")
         # setup: the timed trial blocks of the multi-rank slab path (one call long
         # enough for all of them), 3 x G steps per candidate (G, core pairs, rims)
-        # in {(4,1,A), (8,1,A), (16,1,A), (16,0), (16,2|4,A|B), (16,1,A, other edge_first)}: 372 steps
-        lat.step(400)
+        # in {(4,1,A), (8,1,A), (16,1,A), (16,0), (16,2|4,A|B), (16,1,A, other edge_first),
+        # (16, exchange in order on A)}: 420 steps
+        lat.step(440)
     # clock settle: untimed batches until settle_ms have passed on rank 0 (every
     # rank runs the same batches: the slab exchanges must pair up)
     phase("settle")

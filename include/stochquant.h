@@ -201,6 +201,15 @@ int sq_phi4_schedule(sq_ctx *ctx, int *core_pairs, int *rims_b, int *tuned);
  * except 0 for one rank's RCCL self-exchange; the timed trials of multi-rank
  * contexts try both; SQ_EDGE_FIRST=0|1 pins it.  Single periodic slab: 0. */
 int sq_phi4_edge_first(sq_ctx *ctx, int *edge_first);
+/* Where a deep-halo block's exchange runs: in_order 1 = in order on the
+ * interior stream between the block's last pair and the next block's first
+ * (no core / rim split, no cross-stream event), 0 = on the exchange stream,
+ * overlapped with the core pairs.  Default: 1 for one rank's RCCL or P2P
+ * self-exchange, 0 for ranks on a link, where the timed trials also try 1;
+ * SQ_XCHG_ON_A=0|1 pins it.  kstaged (P2P): the block's last pair also
+ * writes the next exchange's staging slot (no staging copy); default: with
+ * in_order, SQ_P2P_KSTAGE=0|1 pins it.  Single slab / loopback: 0, 0. */
+int sq_phi4_exchange_stream(sq_ctx *ctx, int *in_order, int *kstaged);
 /* The launch schedule of one deep-halo block (pure host logic, no device
  * needed; the product's phi4_block executes exactly this list): a slab of nz
  * planes with a ghost zone of `ghost` planes (the exchange depth G) running

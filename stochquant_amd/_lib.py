@@ -115,6 +115,7 @@ SIGNATURES = {
     "sq_phi4_ghost": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "sq_phi4_schedule": (ctypes.c_int, [_P, _I, _I, _I]),
     "sq_phi4_edge_first": (ctypes.c_int, [_P, _I]),
+    "sq_phi4_exchange_stream": (ctypes.c_int, [_P, _I, _I]),
     "sq_phi4_block_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, ctypes.POINTER(SqBlockOp), ctypes.c_int, _I]),
     "sq_phi4_pick_ghost": (ctypes.c_int, [_D, ctypes.c_int]),

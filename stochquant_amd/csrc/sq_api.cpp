@@ -112,6 +112,7 @@ struct P2pBlob {  // sq_p2p_handle's output
     // the block schedule: pinned settings and which of them the timed pick may
     // change (the pick's candidate list and every exchange depend on them)
     int ef_auto, k_auto, edge_first, core_pairs, rims_b;
+    int a_auto, on_a, kstage;  // the exchange's stream and the staged last pair (SQ_XCHG_ON_A, SQ_P2P_KSTAGE)
     long long Lz, coll_cap;
     unsigned long long seed;
     hipIpcMemHandle_t stage, mbox, coll;
@@ -283,7 +284,12 @@ struct sq_ctx {
     // the slot holds the current field's edges (dropped when anything else
     // writes the field); evE_stale: EDGES_DONE was not recorded behind that
     // pair, so an exchange of the old form records it first
-    bool p2p_kstage = false;
+    // P2P, SQ_XCHG_ON_A=1: the exchange (staging, hand-shake, pull) runs on the
+    // interior stream in order, between a block's last pair and the next
+    // block's first (no core / rim split, no cross-stream event or spin)
+    bool xchg_on_a = false;
+    bool a_auto = true;   // multi-rank timed pick also tries it (unless SQ_XCHG_ON_A pins it)
+    int kstage_env = -1;  // SQ_P2P_KSTAGE if set; else kstage follows xchg_on_a
     unsigned int *kstage_ctr = nullptr;
     unsigned int kstage_n = 0;
     bool kstage_pending = false, kstage_next = false, kstage_issued = false, evE_stale = false;
@@ -840,6 +846,11 @@ int gate_pattern(const std::vector<sq_block_op> &ops) {
     return -1;
 }
 
+// P2P: does the block's last pair write the next exchange's staging slot
+// (SQ_P2P_KSTAGE pins it; by default with the exchange on stream A, whose
+// stream order replaces the count wait on stream B)
+bool kstage_on(const sq_ctx *c) { return c->kstage_env >= 0 ? c->kstage_env != 0 : c->xchg_on_a; }
+
 // Deep-halo block of g <= gz steps on every slab: executes block_plan.
 int phi4_block(sq_ctx *c, int g) {
     const size_t plane = plane_floats(c);
@@ -862,11 +873,17 @@ int phi4_block(sq_ctx *c, int g) {
     // P2P with the staging slot already written by the previous block's last
     // pair (kstage): no EDGES_DONE wait and no staging copy on stream B, the
     // hand-shake waits for that pair's block count instead
-    const bool kst = c->p.comm == SQ_COMM_P2P && c->kstage_pending && ns == 1 && c->p2p_kernel_handshake;
+    // SQ_XCHG_ON_A: the whole exchange on stream A, in order (no events)
+    const bool on_a = c->xchg_on_a && ns == 1 &&
+                      ((c->p.comm == SQ_COMM_P2P && c->p2p_kernel_handshake) || c->p.comm == SQ_COMM_RCCL);
+    // the staged slot is used on stream A (stream order) or, when pinned
+    // (SQ_P2P_KSTAGE=1), on stream B behind a wait for the pair's block count
+    const bool kst = c->p.comm == SQ_COMM_P2P && c->kstage_pending && ns == 1 && c->p2p_kernel_handshake &&
+                     (on_a || c->kstage_env == 1);
     c->kstage_pending = false;
     for (int i = 0; i < ns; ++i) {
         Slab &s = c->slabs[i];
-        if (kst) continue;
+        if (kst || on_a) continue;
         if (c->evE_stale) {  // the last pair before is complete in stream-A order: record it now
             SQ_HIP(hipEventRecord(s.evE, s.sA));
             c->evE_stale = false;
@@ -897,8 +914,9 @@ int phi4_block(sq_ctx *c, int g) {
         // both ranges in one two-range copy launch (a 2-D hipMemcpy ran as a
         // rect-copy kernel of 23 us against 2 x 6 for two linear copies,
         // profiles/r06/c6/tr_p2p)
-        SQ_HIP(sq::p2p_copy2_launch(stg, src_lo[i], stg + (size_t)G * plane, src_hi[i], (size_t)G * plane, s.sB));
-        if (staged_wait) SQ_HIP(hipEventRecord(s.evS, s.sB));
+        SQ_HIP(sq::p2p_copy2_launch(stg, src_lo[i], stg + (size_t)G * plane, src_hi[i], (size_t)G * plane,
+                                    on_a ? s.sA : s.sB));
+        if (staged_wait && !on_a) SQ_HIP(hipEventRecord(s.evS, s.sB));
         src_lo[i] = stg;
         src_hi[i] = stg + (size_t)G * plane;
     }
@@ -929,12 +947,15 @@ int phi4_block(sq_ctx *c, int g) {
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
         const unsigned int e = ++c->xchg_seq;
         const size_t n = (size_t)G * plane;
+        hipStream_t xs = on_a ? s.sA : s.sB;
         if (c->p2p_kernel_handshake) {
             // one wave: "staged e" to both neighbours, then wait for both of theirs
+            // (kstage on stream B: first for the last pair's block count; on
+            // stream A that pair is complete in stream order)
             SQ_HIP(sq::p2p_handshake_launch(c->peers[up].mbox + kMbStagedFromDn, c->peers[dn].mbox + kMbStagedFromUp,
                                             c->mbox + kMbStagedFromDn, c->mbox + kMbStagedFromUp, e,
-                                            kHandshakePolls, c->gate_err, s.sB, kst ? c->kstage_ctr : nullptr,
-                                            c->kstage_n));
+                                            kHandshakePolls, c->gate_err, xs,
+                                            (kst && !on_a) ? c->kstage_ctr : nullptr, c->kstage_n));
         } else {  // stream-ordered flag writes and waits (SQ_P2P_STREAMOPS=1)
             SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[up].mbox + kMbStagedFromDn, e, 0));
             SQ_HIP(hipStreamWriteValue32(s.sB, c->peers[dn].mbox + kMbStagedFromUp, e, 0));
@@ -943,8 +964,8 @@ int phi4_block(sq_ctx *c, int g) {
         }
         // both neighbours' staged copies, pulled by one launch
         SQ_HIP(sq::p2p_copy2_launch(p0 - n, c->peers[dn].stage + slot + n, p0 + (size_t)s.nz * plane,
-                                    c->peers[up].stage + slot, n, s.sB));
-        SQ_HIP(hipEventRecord(s.evC, s.sB));
+                                    c->peers[up].stage + slot, n, xs));
+        if (!on_a) SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     } else {  // RCCL: one slab per process; this send/recv order pairs correctly for P = 2 too
         Slab &s = c->slabs[0];
@@ -952,13 +973,14 @@ int phi4_block(sq_ctx *c, int g) {
         const int P = c->p.nranks, r = c->p.rank;
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
         const size_t n = (size_t)G * plane;
+        hipStream_t xs = on_a ? s.sA : s.sB;
         SQ_NCCLW(c, ncclGroupStart());
-        SQ_NCCLW(c, ncclSend(src_hi[0], n, ncclFloat32, up, c->comm, s.sB));
-        SQ_NCCLW(c, ncclSend(src_lo[0], n, ncclFloat32, dn, c->comm, s.sB));
-        SQ_NCCLW(c, ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, s.sB));
-        SQ_NCCLW(c, ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, s.sB));
+        SQ_NCCLW(c, ncclSend(src_hi[0], n, ncclFloat32, up, c->comm, xs));
+        SQ_NCCLW(c, ncclSend(src_lo[0], n, ncclFloat32, dn, c->comm, xs));
+        SQ_NCCLW(c, ncclRecv(p0 - n, n, ncclFloat32, dn, c->comm, xs));
+        SQ_NCCLW(c, ncclRecv(p0 + (size_t)s.nz * plane, n, ncclFloat32, up, c->comm, xs));
         SQ_NCCLW(c, ncclGroupEnd());
-        SQ_HIP(hipEventRecord(s.evC, s.sB));
+        if (!on_a) SQ_HIP(hipEventRecord(s.evC, s.sB));
         c->perf.halo_bytes += 2.0 * (double)gbytes;
     }
     // gated pair 0: the exchange's completion as a device word the rim chunks poll
@@ -1018,7 +1040,7 @@ int phi4_block(sq_ctx *c, int g) {
                 // P2P kstage: the block's last pair (the whole slab, right before
                 // EDGES_DONE) also writes the next exchange's staging slot
                 c->kstage_issued = false;
-                c->kstage_next = p2p && c->p2p_kstage && ns == 1 && c->p2p_kernel_handshake && !c->in_frame &&
+                c->kstage_next = p2p && kstage_on(c) && ns == 1 && c->p2p_kernel_handshake && !c->in_frame &&
                                  s.stage != nullptr && op.kind == SQ_OP_PAIR && op.stream == kA && op.lo == 0 &&
                                  op.hi == s.nz && op.lo2 >= op.hi2 && oi + 1 < ops.size() &&
                                  ops[oi + 1].kind == SQ_OP_EDGES_DONE && ops[oi + 1].stream == kA;
@@ -1034,7 +1056,7 @@ int phi4_block(sq_ctx *c, int g) {
             } else if (op.kind == SQ_OP_WAIT_EXCHANGE) {
                 if (op.stream != kB) xchg_live = false;
                 // (SQ_DIAG_NO_XWAIT=1, timing diagnostics only: no wait, the rims race the exchange)
-                if (op.stream != kB && !c->diag_no_xwait) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));
+                if (op.stream != kB && !c->diag_no_xwait && !on_a) SQ_HIP(hipStreamWaitEvent(st, s.evC, 0));
                 if (c->p.comm == SQ_COMM_LOOPBACK) {
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + ns - 1) % ns].evC, 0));
                     SQ_HIP(hipStreamWaitEvent(st, c->slabs[(i + 1) % ns].evC, 0));
@@ -1047,6 +1069,8 @@ int phi4_block(sq_ctx *c, int g) {
                     c->kstage_pending = true;
                     c->evE_stale = true;
                     c->kstage_issued = false;
+                } else if (on_a) {  // the next exchange follows on stream A in order
+                    c->evE_stale = true;
                 } else if (!c->stop_used && !c->diag_no_ewait) {
                     SQ_HIP(hipEventRecord(s.evE, st));  // else bound to the pair before
                     c->evE_stale = false;
@@ -1114,25 +1138,28 @@ int gate_reset(sq_ctx *c) {
 int phi4_autotune(sq_ctx *c, int &n) {
     struct Cand {
         int g, k;
-        bool rb, ef;
+        bool rb, ef, a;
     };
     std::vector<Cand> cand;
-    const bool ef = c->edge_first;
+    const bool ef = c->edge_first, a0 = c->xchg_on_a;
     for (int g : {4, 8, 16})
-        if (g <= c->gpad) cand.push_back({g, c->core_pairs, c->rims_b, ef});
-    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs, c->rims_b, ef});
+        if (g <= c->gpad) cand.push_back({g, c->core_pairs, c->rims_b, ef, a0});
+    if (cand.empty()) cand.push_back({c->gpad, c->core_pairs, c->rims_b, ef, a0});
     const int gd = cand.back().g;
-    if (c->tbz > 0 && c->k_auto) {
-        cand.push_back({gd, 0, false, ef});
+    if (c->tbz > 0 && c->k_auto && !a0) {
+        cand.push_back({gd, 0, false, ef, false});
         for (bool rb : {false, true})
             for (int k : {2, 4})
-                if (k <= gd / 2) cand.push_back({gd, k, rb, ef});
+                if (k <= gd / 2) cand.push_back({gd, k, rb, ef, false});
     }
+    // the exchange in order on stream A (no overlap, no cross-stream hop):
+    // cheaper when the transfer is short, so timed like the rest
+    if (c->a_auto && !a0) cand.push_back({gd, 0, false, ef, true});
     // the edges-first split of the block's last pair buys the next exchange a
     // longer window at the price of a split launch and an event bubble: worth
     // it when the exchange is long (a real link), not on one GPU (19.3 vs 19.9
     // us/step at 256^3, profiles/r03/s2/slab_ef/), so both are timed
-    if (c->ef_auto) cand.push_back({gd, c->core_pairs, c->rims_b, !ef});
+    if (c->ef_auto) cand.push_back({gd, c->core_pairs, c->rims_b, !ef, a0});
     if (cand.size() > 16) cand.resize(16);  // dtune holds 16 times
     int need = 0;
     for (const Cand &k : cand) need += 3 * k.g;
@@ -1147,6 +1174,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
         c->core_pairs = cand[k].k;
         c->rims_b = cand[k].rb;
         c->edge_first = cand[k].ef;
+        c->xchg_on_a = cand[k].a;
         int rc = phi4_block(c, g);
         if (!rc) rc = phi4_join(c);
         if (rc) return rc;
@@ -1177,6 +1205,7 @@ int phi4_autotune(sq_ctx *c, int &n) {
     c->core_pairs = best.k;
     c->rims_b = best.rb;
     c->edge_first = best.ef;
+    c->xchg_on_a = best.a;
     c->g_tuned = true;
     return SQ_OK;
 }
@@ -1468,7 +1497,18 @@ int create_phi4(sq_ctx *c) {
         SQ_HIP(hipMalloc(&c->kstage_ctr, 64));
         SQ_HIP(hipMemset(c->kstage_ctr, 0, 64));
         const char *ks = getenv("SQ_P2P_KSTAGE");
-        c->p2p_kstage = ks ? atoi(ks) != 0 : false;
+        if (ks) c->kstage_env = atoi(ks) != 0 ? 1 : 0;
+    }
+    if (p.comm == SQ_COMM_P2P || p.comm == SQ_COMM_RCCL) {
+        // one rank's self-exchange moves no bytes over a link: in order on the
+        // interior stream it costs less than the two cross-stream hops that
+        // overlap it (RCCL 1.117 vs 1.148, P2P with the staged last pair 1.078
+        // vs 1.142 x the single slab, profiles/r06/c25); ranks on a link get
+        // it as one more candidate of the timed pick (phi4_autotune)
+        if (const char *xa = getenv("SQ_XCHG_ON_A")) {
+            c->xchg_on_a = atoi(xa) != 0;
+            c->a_auto = false;
+        }
     }
     if (p.comm == SQ_COMM_P2P) {  // mailbox and collective slots; peers mapped by sq_p2p_connect
         // fine-grained device memory: the words are written by the peers'
@@ -1517,6 +1557,15 @@ int create_phi4(sq_ctx *c) {
     }
     if (const char *e = getenv("SQ_RIMS_B")) {
         c->rims_b = atoi(e) != 0;
+        c->k_auto = false;
+    }
+    // one rank's self-exchange: in order on stream A unless pinned otherwise
+    // (SQ_XCHG_ON_A, or a pinned core / rim split)
+    if ((p.comm == SQ_COMM_P2P || p.comm == SQ_COMM_RCCL) && p.nranks == 1 && c->a_auto && c->k_auto)
+        c->xchg_on_a = true;
+    if (c->xchg_on_a) {  // the exchange runs between two pairs on stream A: nothing to split around it
+        c->core_pairs = 0;
+        c->rims_b = false;
         c->k_auto = false;
     }
     c->zc = zc;
@@ -2675,6 +2724,15 @@ int sq_phi4_edge_first(sq_ctx *c, int *edge_first) {
     return SQ_OK;
 }
 
+int sq_phi4_exchange_stream(sq_ctx *c, int *in_order, int *kstaged) {
+    if (!c) return fail(SQ_E_ARG, "null context");
+    if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
+    const bool slab = c->p.comm == SQ_COMM_P2P || c->p.comm == SQ_COMM_RCCL;
+    if (in_order) *in_order = slab && c->xchg_on_a ? 1 : 0;
+    if (kstaged) *kstaged = c->p.comm == SQ_COMM_P2P && kstage_on(c) ? 1 : 0;
+    return SQ_OK;
+}
+
 int sq_phi4_stability(sq_ctx *c, double state[2], int *fired_step, float *M, float *D, float *A, int n) {
     if (!c) return fail(SQ_E_ARG, "null context");
     if (!is_phi4(c)) return fail(SQ_E_STATE, "PHI4 only");
@@ -3015,6 +3073,9 @@ int sq_p2p_handle(sq_ctx *c, unsigned char out[SQ_P2P_HANDLE_BYTES]) {
     b.edge_first = c->edge_first ? 1 : 0;
     b.core_pairs = c->core_pairs;
     b.rims_b = c->rims_b ? 1 : 0;
+    b.a_auto = c->a_auto ? 1 : 0;
+    b.on_a = c->xchg_on_a ? 1 : 0;
+    b.kstage = c->kstage_env;
     b.Lz = c->Lz;
     b.coll_cap = (long long)c->coll_cap;
     b.seed = c->p.seed;
@@ -3049,9 +3110,10 @@ int sq_p2p_connect(sq_ctx *c, const unsigned char *handles, int nranks) {
             return fail(SQ_E_ARG, "rank " + std::to_string(q) + " has different loops (" + std::to_string(b.loops) +
                                       "), active ghost depth (" + std::to_string(b.gz) + ") or ghost tuning (SQ_GHOST)");
         if (b.ef_auto != (c->ef_auto ? 1 : 0) || b.k_auto != (c->k_auto ? 1 : 0) ||
-            b.edge_first != (c->edge_first ? 1 : 0) || b.core_pairs != c->core_pairs || b.rims_b != (c->rims_b ? 1 : 0))
+            b.edge_first != (c->edge_first ? 1 : 0) || b.core_pairs != c->core_pairs || b.rims_b != (c->rims_b ? 1 : 0) ||
+            b.a_auto != (c->a_auto ? 1 : 0) || b.on_a != (c->xchg_on_a ? 1 : 0) || b.kstage != c->kstage_env)
             return fail(SQ_E_ARG, "rank " + std::to_string(q) + " has a different block schedule (SQ_EDGE_FIRST, "
-                                      "SQ_CORE_PAIRS, SQ_RIMS_B must be set alike on every rank)");
+                                      "SQ_CORE_PAIRS, SQ_RIMS_B, SQ_XCHG_ON_A, SQ_P2P_KSTAGE must be set alike on every rank)");
     }
     DeviceGuard g(c->dev);
     for (int q = 0; q < nranks; ++q) {

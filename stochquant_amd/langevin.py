@@ -301,12 +301,15 @@ class Phi4Lattice(_Ctx):
 
     @property
     def schedule(self):
-        """{"ghost", "core_pairs", "rims_b", "edge_first", "tuned"} of a slab decomposition's block schedule."""
+        """{"ghost", "core_pairs", "rims_b", "edge_first", "tuned", "exchange_in_order", "kstaged"} of a slab
+        decomposition's block schedule (sq_phi4_schedule, sq_phi4_edge_first, sq_phi4_exchange_stream)."""
         k, b, t, e = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.call("sq_phi4_schedule", self._h, ctypes.byref(k), ctypes.byref(b), ctypes.byref(t))
         _lib.call("sq_phi4_edge_first", self._h, ctypes.byref(e))
+        a, ks = ctypes.c_int(), ctypes.c_int()
+        _lib.call("sq_phi4_exchange_stream", self._h, ctypes.byref(a), ctypes.byref(ks))
         return {"ghost": self.ghost[0], "core_pairs": k.value, "rims_b": bool(b.value), "edge_first": bool(e.value),
-                "tuned": bool(t.value)}
+                "tuned": bool(t.value), "exchange_in_order": bool(a.value), "kstaged": bool(ks.value)}
 
     def save(self, path):
         """Binary checkpoint: <path> (.npy float32 (nz, Ly, Lx)) + <path>.json (step, dtau, seed, z0)."""

@@ -118,8 +118,9 @@ def test_p2p_single_rank_in_process(gpu):
         assert np.array_equal(L.download(), mono["field"][0])
 
 
+@pytest.mark.parametrize("on_a", ["0", "1"])
 @pytest.mark.parametrize("ghost", ["4", "16"])
-def test_p2p_single_rank_kernel_staged(gpu, monkeypatch, ghost):
+def test_p2p_single_rank_kernel_staged(gpu, monkeypatch, ghost, on_a):
     """P = 1 with SQ_P2P_KSTAGE=1: several step calls (each block's last pair
     stages the next exchange, across calls too), an upload in between (the
     staged edges are dropped and re-staged by copy), a frame (frames stage by
@@ -131,6 +132,7 @@ def test_p2p_single_rank_kernel_staged(gpu, monkeypatch, ghost):
               ("frame", None), ("step", 24), ("field", None)]
     mono = _mono(shape, kw, script)
     monkeypatch.setenv("SQ_P2P_KSTAGE", "1")
+    monkeypatch.setenv("SQ_XCHG_ON_A", on_a)
     monkeypatch.setenv("SQ_GHOST", ghost)
     got = []
     with _lat(shape, comm="p2p", nranks=1, rank=0, **kw) as L:
@@ -177,6 +179,11 @@ def test_p2p_unconnected_context_refuses_to_step(gpu):
     (2, (256, 16, 64), 30, {"SQ_GHOST": "16", "SQ_CORE_PAIRS": "0", "SQ_P2P_KSTAGE": "1"}),
     (8, (256, 16, 256), 40, {"SQ_GHOST": "8", "SQ_CORE_PAIRS": "2", "SQ_P2P_KSTAGE": "1"}),
     (4, (256, 8, 20), 33, {"SQ_GHOST": "4", "SQ_P2P_KSTAGE": "1"}),  # slabs of 5 planes: edges overlap
+    # the exchange in order on the interior stream (SQ_XCHG_ON_A=1), by copy or kernel-staged
+    (2, (256, 16, 64), 21, {"SQ_GHOST": "8", "SQ_XCHG_ON_A": "1"}),
+    (4, (32, 8, 32), 9, {"SQ_GHOST": "2", "SQ_XCHG_ON_A": "1"}),
+    (3, (256, 16, 96), 40, {"SQ_GHOST": "8", "SQ_XCHG_ON_A": "1", "SQ_P2P_KSTAGE": "1"}),
+    (8, (256, 16, 256), 40, {"SQ_GHOST": "16", "SQ_XCHG_ON_A": "1", "SQ_P2P_KSTAGE": "1"}),
 ])
 def test_p2p_ranks_bitwise_vs_single_slab(gpu, nranks, shape, steps, env):
     phi0 = _field0(shape)
@@ -195,7 +202,7 @@ def test_p2p_ghost_trials_agree_across_ranks(gpu):
     the same schedule, and the trial steps are ordinary steps."""
     shape = (256, 16, 128)
     phi0 = _field0(shape)
-    script = [("upload", phi0), ("step", 390), ("ghost", None), ("field", None)]
+    script = [("upload", phi0), ("step", 430), ("ghost", None), ("field", None)]
     mono = _mono(shape, KW, script)
     outs = run_ranks(2, shape, KW, script)
     assert outs[0]["ghost"] == outs[1]["ghost"] and outs[0]["ghost"][0] in (4, 8, 16)

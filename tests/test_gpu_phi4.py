@@ -482,6 +482,41 @@ def test_core_pairs_ahead_of_the_exchange_bitwise(gpu, oracle_mod, monkeypatch, 
             assert np.array_equal(L.download(), mono), kw["comm"]
 
 
+@pytest.mark.parametrize("ghost", ["4", "16"])
+@pytest.mark.parametrize("kstage", ["0", "1"])
+def test_exchange_on_interior_stream_bitwise(gpu, oracle_mod, monkeypatch, ghost, kstage):
+    """SQ_XCHG_ON_A=1: the exchange (RCCL send / recv; P2P staging, hand-shake
+    and pull, the staging slot written by the last pair under SQ_P2P_KSTAGE=1)
+    runs in order on the interior stream between a block's last pair and the
+    next block's first: RCCL and P2P self-exchange == the single slab, bit for
+    bit, over full and partial blocks and a frame in between."""
+    from stochquant_amd import unique_id
+    shape = (256, 16, 96)
+    phi0 = _init(oracle_mod, shape)
+    with _lat(shape, loops=6) as L:
+        L.upload(phi0)
+        L.step(16)
+        L.step(21)
+        ok = L.run_frame()
+        L.step(9)
+        mono = L.download()
+    monkeypatch.setenv("SQ_XCHG_ON_A", "1")
+    monkeypatch.setenv("SQ_P2P_KSTAGE", kstage)
+    monkeypatch.setenv("SQ_GHOST", ghost)
+    monkeypatch.setenv("SQ_FUSE2", "1")
+    for kw in (dict(comm="rccl", nranks=1, rank=0, comm_id=unique_id()), dict(comm="p2p", nranks=1, rank=0)):
+        with _lat(shape, loops=6, **kw) as L:
+            if kw["comm"] == "p2p":
+                L.p2p_connect([L.p2p_handle()])
+            assert L.schedule["core_pairs"] == 0
+            L.upload(phi0)
+            L.step(16)
+            L.step(21)
+            assert L.run_frame() == ok
+            L.step(9)
+            assert np.array_equal(L.download(), mono), kw["comm"]
+
+
 def test_fused_two_step_rccl_frames(gpu, oracle_mod, monkeypatch):
     """RCCL self-exchange slab with fused inner steps, run as frames."""
     from stochquant_amd import unique_id
@@ -664,13 +699,17 @@ def test_slice_correlator_across_slabs(gpu, oracle_mod):
         assert np.array_equal(L.correlator(24), mono)
 
 
-@pytest.mark.parametrize("comm", ["loopback", "rccl"])
+@pytest.mark.parametrize("comm", ["loopback", "rccl", "rccl_overlap"])
 def test_ghost_autotune_is_exact(gpu, oracle_mod, monkeypatch, comm):
     """Timed trial blocks pick G in {4, 8, 16} and the core pairs that run
-    ahead of the exchange in {1, 2, 4}; the trial steps are ordinary steps, so
-    the field after them equals the single-slab run bit for bit."""
+    ahead of the exchange in {1, 2, 4} (rccl_overlap: the exchange pinned to
+    its own stream; rccl: one rank's default, the exchange in order on the
+    interior stream); the trial steps are ordinary steps, so the field after
+    them equals the single-slab run bit for bit."""
     from stochquant_amd import unique_id
     monkeypatch.setenv("SQ_GHOST_AUTO", "1")
+    if comm == "rccl_overlap":
+        monkeypatch.setenv("SQ_XCHG_ON_A", "0")
     shape = (256, 8, 128)
     phi0 = _init(oracle_mod, shape)
     steps = 390            # >= 3*(4+8+16) + 6*3*16 = 372 trial steps, then 18 more
