@@ -2358,6 +2358,10 @@ int sq_destroy(sq_ctx *c) {
         hipStream_t sB = c->slabs[0].sB;
         const int P = c->p.nranks, r = c->p.rank;
         const int up = (r + 1) % P, dn = (r + P - 1) % P;
+        // with the exchange in order on stream A (SQ_XCHG_ON_A) our last pulls
+        // ran there: the acknowledgements on stream B must follow them (the
+        // hand-shake's bounded poll ends stream A's work even if a peer died)
+        (void)hipStreamSynchronize(c->slabs[0].sA);
         if (hipStreamWriteValue32(sB, c->peers[dn].mbox + kMbAckFromUp, c->xchg_seq, 0) != hipSuccess ||
             hipStreamWriteValue32(sB, c->peers[up].mbox + kMbAckFromDn, c->xchg_seq, 0) != hipSuccess ||
             wait_seq(sB, c->mbox + kMbAckFromDn, c->xchg_seq) != hipSuccess ||
