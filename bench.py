@@ -742,8 +742,10 @@ def frames_record(a, local, nframes=200, loops=20, rounds=8):
 def slab_record(a, local, steps=1000, rounds=5):
     """SURVEY §8e's slab path on one GPU: the 256^3 lattice as one z-slab whose
     halo exchange goes through the product's transports to itself (RCCL
-    self-exchange; P2P peer pointers), G = 16 deep halos, fused pairs, the
-    exchange on stream B -- per-step time against the single periodic slab in
+    self-exchange; P2P peer pointers), G = 16 deep halos, fused pairs, one
+    rank's default schedule (the exchange in order on the interior stream
+    between blocks, P2P's last pair writing its staging slot; DESIGN.md §8.3,
+    reported as each context's "schedule") -- per-step time against the single periodic slab in
     the same run (the ratio is what the exchange machinery costs before any
     xGMI).  All three contexts stay open and are timed in turn, `rounds` times
     `steps` steps each after 2000 warm-up steps, medians: one measurement per
@@ -1050,7 +1052,9 @@ def run(a, world, rank, watch):
                 "block_schedule": schedule,
                 "parallelism": "single GPU, one stream" if not slab_path else
                                f"z-slab x{world} ({a.comm if world == 1 or a.comm == 'p2p' else a.transport}), halo "
-                               f"exchange on stream B, interior on stream A",
+                               + ("exchange in order on the interior stream between blocks"
+                                  if (schedule or {}).get("exchange_in_order") else
+                                  "exchange on stream B, interior on stream A"),
             },
             "transport_fallback": a.transport_fallback,
             "roofline": rl,
