@@ -23,7 +23,7 @@
 extern "C" {
 #endif
 
-#define SQ_ABI_VERSION 5
+#define SQ_ABI_VERSION 6
 
 /* status codes */
 #define SQ_OK 0

@@ -79,7 +79,7 @@ class SqBlockOp(ctypes.Structure):
 
 (SQ_OP_EXCHANGE, SQ_OP_STEP, SQ_OP_PAIR, SQ_OP_WAIT_EXCHANGE, SQ_OP_EDGES_DONE, SQ_OP_WAIT_STAGED, SQ_OP_SIGNAL,
  SQ_OP_WAIT) = range(8)
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 _P = ctypes.c_void_p

@@ -36,7 +36,7 @@ def test_params_layout_and_defaults(sqlib):
     assert p.struct_size == ctypes.sizeof(_lib.SqParams)
     assert p.clamp == 1000.0          # tau_kernel.cl:61
     assert p.adapt_dtau == 1          # tauhost.c:523-541
-    assert sqlib.sq_abi_version() == _lib.ABI_VERSION == 5
+    assert sqlib.sq_abi_version() == _lib.ABI_VERSION == 6
 
 
 def test_no_silent_cpu_fallback(sqlib):
