@@ -19,7 +19,15 @@ an adversarial scheduler advances any rank whose next operation is enabled
 must find exactly the exchange it expects -- for P = 1 (a rank is its own
 neighbour), P = 2 (both neighbours one peer) and larger rings, thousands of
 schedules each.  The same model with ONE slot fails, which shows the checker
-can see the hazard the second slot removes."""
+can see the hazard the second slot removes.
+
+The same program covers round 6's later forms: with the exchange in order on
+the interior stream (SQ_XCHG_ON_A) every operation is on that one stream in
+this order, and with the staged last pair (SQ_P2P_KSTAGE) the "copy" of
+exchange e is the block's last pair writing slot e & 1, which that stream runs
+after the pulls of exchange e - 1 (the exchange stream's form: its hand-shake
+waits for the pair's block count, and the pair follows the rim pair that
+waited for those pulls) -- the order the model checks."""
 import random
 
 import pytest
